@@ -1,0 +1,146 @@
+/*
+ * vss.h — C ABI of the MI355X-native VSS (IEEE Very Small Size, 3v3) match step.
+ *
+ * This is the drop-in boundary for the hot path named by BASELINE.json `north_star`:
+ * the reference's `VSS.step` (envs/vss.py:180-333 + the Ext IsaacGymEnvs VecTask.step that
+ * drives it, + PhysX `gym.simulate`) and the SA/CMA/DMA wrapper packing
+ * (envs/wrappers.py:5-19,89-180).  The Python classes in
+ * `rsoccer-isaac-cleanrl_amd/envs/{vss,wrappers}.py` bind these entry points with ctypes.
+ *
+ * Conventions:
+ *   - every buffer is a caller-owned DEVICE allocation (torch tensors); the library allocates
+ *     nothing and keeps no hidden state besides what is passed in;
+ *   - all work is enqueued on `stream` (a hipStream_t passed as void*); no host synchronisation;
+ *   - return value 0 = ok, otherwise a VSS_E_* code (vss_error_string() describes it);
+ *   - runtime parameters (reward weights, episode length, clip, seed) are passed per call.
+ *
+ * Field state layout (struct-of-arrays, fp32, `state[channel * n_fields + field]`), chosen so
+ * the reference's tensor views (envs/vss.py:112-132) are plain strided views of one buffer:
+ *   VSS_CH_BALL_X..VSS_CH_BALL_VY             ball x, y, vx, vy
+ *   VSS_CH_RX + r, VSS_CH_RY + r               robot r position      (r = team*3 + robot)
+ *   VSS_CH_RQX..VSS_CH_RQW + r                 robot r quaternion x,y,z,w (x,y unused: planar)
+ *   VSS_CH_RVX + r, VSS_CH_RVY + r             robot r linear velocity
+ *   VSS_CH_RW + r                              robot r yaw rate
+ */
+#ifndef VSS_AMD_VSS_H
+#define VSS_AMD_VSS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VSS_ABI_VERSION 1
+
+#define VSS_NUM_TEAMS 2          /* envs/vss.py:24 */
+#define VSS_NUM_ROBOTS 3         /* envs/vss.py:25 */
+#define VSS_NUM_AGENTS 6
+#define VSS_NUM_OBS 52           /* envs/vss.yaml:4, layout envs/vss.py:530-575 */
+#define VSS_NUM_ACTIONS 2        /* envs/vss.yaml:5 (left wheel, right wheel) */
+#define VSS_NUM_REW 4            /* goal, grad, move, energy: envs/vss.py:90-92 */
+
+/* state channels */
+#define VSS_CH_BALL_X 0
+#define VSS_CH_BALL_Y 1
+#define VSS_CH_BALL_VX 2
+#define VSS_CH_BALL_VY 3
+#define VSS_CH_RX 4
+#define VSS_CH_RY 10
+#define VSS_CH_RQX 16
+#define VSS_CH_RQY 22
+#define VSS_CH_RQZ 28
+#define VSS_CH_RQW 34
+#define VSS_CH_RVX 40
+#define VSS_CH_RVY 46
+#define VSS_CH_RW 52
+#define VSS_STATE_CHANNELS 58
+
+/* which wrapper the step is fused with (envs/wrappers.py:43-48) */
+#define VSS_MODE_FULL 0  /* raw VSS.step: actions (N,2,3,2), obs (N,2,3,52), rew (N,2,3,4) */
+#define VSS_MODE_SA 1    /* SingleAgent: learner = blue robot 0 (envs/wrappers.py:89-115)   */
+#define VSS_MODE_CMA 2   /* CMA: learner = blue team, one 6-vector (envs/wrappers.py:118-148) */
+#define VSS_MODE_DMA 3   /* DMA: learner = blue robots 0..2, one row each (wrappers.py:151-180) */
+
+/* error codes */
+#define VSS_OK 0
+#define VSS_E_ARG 1      /* null pointer / bad size / bad mode */
+#define VSS_E_LAUNCH 2   /* kernel launch failed (hipGetLastError) */
+
+typedef struct vss_params {
+  float w_goal;              /* rew_weights.goal   envs/vss.yaml:9,  envs/vss.py:44 */
+  float w_grad;              /* rew_weights.grad   envs/vss.yaml:10 */
+  float w_move;              /* rew_weights.move   envs/vss.yaml:11 */
+  float w_energy;            /* rew_weights.energy envs/vss.yaml:12 */
+  float clip_actions;        /* env.clipActions    envs/vss.yaml:7 (Ext VecTask clamp) */
+  int32_t max_episode_length;/* env.maxEpisodeLength envs/vss.yaml:6 */
+  uint64_t seed;             /* Philox key for reset sampling and OU noise */
+} vss_params;
+
+typedef struct vss_state {
+  float* state;              /* [VSS_STATE_CHANNELS][n_fields] fp32 SoA (see above)       */
+  int64_t* progress_buf;     /* [n_fields]   envs/vss.py:95                               */
+  int64_t* reset_buf;        /* [n_fields]   envs/vss.py:93                               */
+  float* dof_velocity_buf;   /* [n_fields][2][3][2] last clamped actions, envs/vss.py:137  */
+  uint32_t* rng_counter;     /* [n_fields]   per-field Philox step counter                */
+} vss_state;
+
+/*
+ * Per-step inputs/outputs.  Shapes by mode (N = n_fields, R = 3 for DMA else 1):
+ *   actions      FULL (N,2,3,2) | SA (N,2) | CMA (N,6) | DMA (3N,2)             read
+ *   ou_buf       wrapper action buffer (N,2,3,2); SA/CMA/DMA only                 read+write
+ *   obs          FULL (N,2,3,52) | SA/CMA (N,52) | DMA (3N,52)                     write
+ *   terminal_obs same shape as obs (pre-reset observation)                        write
+ *   rew          FULL (N,2,3,4) | SA/CMA (N,4) | DMA (3N,4)                        write
+ *   reward_sum   SA/CMA (N,) | DMA (3N,) = rews.sum(-1); may be NULL in FULL       write
+ *   dones_rep    DMA only: (3N,) int64 = dones.repeat_interleave(3); else NULL     write
+ *   time_outs    (R*N,) uint8 (torch.bool)                                          write
+ *   progress_f   (R*N,) fp32 = progress_buf.float() before the reset              write
+ */
+typedef struct vss_step_io {
+  const float* actions;
+  float* ou_buf;
+  float* obs;
+  float* terminal_obs;
+  float* rew;
+  float* reward_sum;
+  int64_t* dones_rep;
+  uint8_t* time_outs;
+  float* progress_f;
+} vss_step_io;
+
+/* ABI version (VSS_ABI_VERSION). */
+int vss_abi_version(void);
+
+/* Human-readable text for a VSS_E_* code. */
+const char* vss_error_string(int code);
+
+/*
+ * One control step of every field.  Replaces, for mode FULL, Ext VecTask.step →
+ * VSS.pre_physics_step (envs/vss.py:180-187) → gym.simulate → VSS.post_physics_step
+ * (envs/vss.py:189-203) → time_outs; for SA/CMA/DMA additionally the wrapper's
+ * random_ou + learner overwrite + slicing (envs/wrappers.py:101-115, 133-148, 163-180).
+ */
+int vss_step(void* stream, int64_t n_fields, int32_t mode, const vss_params* params,
+             const vss_state* st, const vss_step_io* io);
+
+/*
+ * Re-sample every field whose reset_buf != 0 (VSS.reset_dones, envs/vss.py:267-333);
+ * callable externally after `reset_buf[:] = 1` (play.py:132-133).  Does not touch
+ * reset_buf / progress_buf and does not compute observations (same as the reference).
+ */
+int vss_reset_dones(void* stream, int64_t n_fields, const vss_params* params,
+                    const vss_state* st);
+
+/*
+ * compute_obs (envs/vss.py:205-216, 530-575) for agents [0, n_agents): n_agents = 6 writes
+ * (N,2,3,52), 3 writes the blue team (N,3,52), 1 writes blue robot 0 (N,52).
+ */
+int vss_compute_observations(void* stream, int64_t n_fields, const vss_state* st,
+                             float* obs, int32_t n_agents);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VSS_AMD_VSS_H */

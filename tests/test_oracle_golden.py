@@ -1,0 +1,205 @@
+"""Pin the CPU oracle against golden vectors produced by the REFERENCE's own Python.
+
+Fixtures: tests/golden/*.npz, made by tests/golden/gen_golden.py (imports /root/reference with
+stub Isaac Gym modules; physics hook = this oracle's physics).  These tests run on CPU.
+Tolerances: integer outputs (goal, dones, progress, time-outs, reset counts) bit-exact; float
+outputs bit-exact except values that go through sin/cos (reference: torch atan2/sin/cos of the
+quaternion; oracle: algebraic cos = w^2 - z^2, sin = 2wz, and polynomial half-angle sin/cos for
+reset yaw), which must agree within 2e-6.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+TRIG_ATOL = 2e-6
+
+
+def load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+
+
+def obs_trig_mask():
+    """(312,) bool: obs features that are cos/sin(yaw) in the (2,3,52) layout."""
+    m = np.zeros(52, bool)
+    for k in range(3):
+        m[4 + 9 * k + 4] = m[4 + 9 * k + 5] = True
+    for k in range(3):
+        m[31 + 7 * k + 4] = m[31 + 7 * k + 5] = True
+    return np.tile(m, 6)
+
+
+def assert_obs_equal(got, want, agents=6):
+    got = got.reshape(-1, agents * 52)
+    want = want.reshape(-1, agents * 52)
+    trig = obs_trig_mask()[: agents * 52]
+    np.testing.assert_array_equal(got[:, ~trig], want[:, ~trig])
+    np.testing.assert_allclose(got[:, trig], want[:, trig], atol=TRIG_ATOL, rtol=0)
+
+
+# --------------------------------------------------------------------------------- G1-G3
+def test_compute_obs_matches_reference(golden_dir):
+    g = load(golden_dir, "g1_g3_kernels.npz")
+    s = g["obs_state"]
+    n = s.shape[1]
+    env = O.HostEnv(n)
+    env.state[:] = s
+    env.dof[:] = g["obs_actions"]
+    obs = O.compute_obs(env, 6)
+    assert_obs_equal(obs, g["obs"])
+    # blue-team (DMA) and blue-robot-0 (SA) packings are prefixes of the full layout
+    np.testing.assert_array_equal(O.compute_obs(env, 3), obs[:, :3])
+    np.testing.assert_array_equal(O.compute_obs(env, 1), obs[:, :1])
+
+
+def test_goal_and_dones_bit_exact(golden_dir):
+    g = load(golden_dir, "g1_g3_kernels.npz")
+    balls = np.ascontiguousarray(g["goal_ball"])
+    m = len(balls)
+    goal = np.zeros(m, np.int64)
+    O.lib().oracle_goal_rew(m, O._p(balls), O._p(goal))
+    want = g["goal"]  # (m, 2, 3): blue +g, yellow -g
+    np.testing.assert_array_equal(want[:, 0, 0], goal)
+    np.testing.assert_array_equal(want[:, 1, 2], -goal)
+    prog = np.ascontiguousarray(g["goal_progress"])
+    dones = np.zeros(m, np.int64)
+    O.lib().oracle_vss_dones(m, O._p(balls), O._p(prog), 400, O._p(dones))
+    np.testing.assert_array_equal(dones, g["dones"])
+    assert dones.sum() > 0 and (dones == 0).sum() > 0
+
+
+def test_grad_move_energy_match_reference(golden_dir):
+    g = load(golden_dir, "g1_g3_kernels.npz")
+    n = len(g["ball"])
+    pb, b = np.ascontiguousarray(g["prev_ball"]), np.ascontiguousarray(g["ball"])
+    grad = np.zeros(n, np.float32)
+    O.lib().oracle_grad_rew(n, O._p(pb), O._p(b), O._p(grad))
+    np.testing.assert_allclose(grad, g["grad"][:, 0, 0], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(-grad, g["grad"][:, 1, 1], rtol=0, atol=1e-6)
+    move = np.zeros((n, 6), np.float32)
+    pr, r = np.ascontiguousarray(g["prev_rob"]), np.ascontiguousarray(g["rob"])
+    O.lib().oracle_move_rew(n, O._p(pr), O._p(r), O._p(pb), O._p(b), O._p(move))
+    np.testing.assert_allclose(move, g["move"].reshape(n, 6), rtol=0, atol=1e-6)
+
+
+# --------------------------------------------------------------------------------- G4
+def _env_from_live(n, live_channels, live_state, progress, reset):
+    env = O.HostEnv(n)
+    env.state[:] = 0
+    env.state[live_channels] = live_state
+    env.progress[:] = progress
+    env.reset[:] = reset
+    return env
+
+
+def test_construction_reset_matches_reference(golden_dir):
+    """VSS.__init__ → reset_dones over all fields (envs/vss.py:72, 267-333), replayed draws."""
+    g = load(golden_dir, "g4_full_rollout.npz")
+    n = g["init_state"].shape[1]
+    env = O.HostEnv(n)
+    draws, keep = O.make_draws(g["init_uniforms"], np.zeros(0, np.float32))
+    O.reset_dones(env, O.params(max_episode_length=int(g["max_len"])), draws)
+    assert draws.uniform_pos == len(g["init_uniforms"]), "reference draw count not reproduced"
+    want = g["init_state"]
+    live = g["live_channels"]
+    quat = np.isin(live, list(range(O.CH_RQZ, O.CH_RQZ + 12)))
+    np.testing.assert_array_equal(env.state[live[~quat]], want[live[~quat]])
+    np.testing.assert_allclose(env.state[live[quat]], want[live[quat]], atol=TRIG_ATOL, rtol=0)
+
+
+def test_full_step_bookkeeping_matches_reference(golden_dir):
+    """Teacher-forced replay of the reference's VSS.step (16 fields x 160 steps by default
+    config of the generator) -- progress / reset / time-out ordering, rewards, terminal obs,
+    reset sampling order, dof zeroing (envs/vss.py:180-333, Ext VecTask.step)."""
+    g = load(golden_dir, "g4_full_rollout.npz")
+    live = g["live_channels"]
+    T, n = g["reset"].shape
+    prm = O.params(max_episode_length=int(g["max_len"]))
+    quat = np.isin(live, list(range(O.CH_RQZ, O.CH_RQZ + 12)))
+    obs_at = {int(t): i for i, t in enumerate(g["obs_steps"])}
+    u_off = np.concatenate([[0], np.cumsum(g["u_count"])])
+    forced = {int(t): i for i, t in enumerate(g["forced_steps"])}
+    for t in range(T):
+        if t == 0:
+            env = O.HostEnv(n)
+            env.state[:] = g["start_state"]
+            env.progress[:] = 0
+            env.reset[:] = 1
+        else:
+            pre = g["forced_state"][forced[t]] if t in forced else g["state"][t - 1]
+            env = _env_from_live(n, live, pre, g["progress"][t - 1], g["reset"][t - 1])
+            env.dof[:] = g["dof"][t - 1]
+        io = O.make_io(n, O.MODE_FULL)
+        draws, keep = O.make_draws(g["uniforms"][u_off[t]:u_off[t + 1]], np.zeros(0, np.float32))
+        O.step(env, O.MODE_FULL, g["actions"][t], io, prm, draws)
+        assert draws.uniform_pos == g["u_count"][t], f"step {t}: draw count"
+        np.testing.assert_array_equal(env.reset, g["reset"][t], err_msg=f"step {t}")
+        np.testing.assert_array_equal(env.progress, g["progress"][t], err_msg=f"step {t}")
+        np.testing.assert_array_equal(io["time_outs"], g["time_outs"][t], err_msg=f"step {t}")
+        np.testing.assert_array_equal(io["progress_f"], g["progress_f"][t], err_msg=f"step {t}")
+        np.testing.assert_array_equal(env.dof, g["dof"][t], err_msg=f"step {t}")
+        np.testing.assert_allclose(io["rew"], g["rew"][t], rtol=1e-6, atol=1e-6, err_msg=f"step {t}")
+        st = env.state[live]
+        np.testing.assert_array_equal(st[~quat], g["state"][t][~quat], err_msg=f"step {t}")
+        np.testing.assert_allclose(st[quat], g["state"][t][quat], atol=TRIG_ATOL, rtol=0, err_msg=f"step {t}")
+        if t in obs_at:
+            assert_obs_equal(io["obs"], g["obs"][obs_at[t]])
+            assert_obs_equal(io["terminal_obs"], g["terminal_obs"][obs_at[t]])
+    assert g["time_outs"].sum() > 0 and (np.abs(g["rew"][:, :, 0]) > 0).sum() > 0
+    # the time-out edge: a goal at progress max_len-1 is a time-out, at max_len-2 it is not
+    ml = int(g["max_len"])
+    t1, t2 = ml - 2, ml - 3
+    assert g["reset"][t1, 2] == 1 and g["time_outs"][t1, 2] == 1 and g["progress"][t1, 2] == ml - 1
+    assert g["reset"][t2, 3] == 1 and g["time_outs"][t2, 3] == 0 and g["progress"][t2, 3] == ml - 2
+
+
+# --------------------------------------------------------------------------------- G5
+@pytest.mark.parametrize("mode_name", ["sa", "cma", "dma"])
+def test_wrapped_step_matches_reference(golden_dir, mode_name):
+    """SingleAgent / CMA / DMA (envs/wrappers.py:5-19, 89-180), teacher-forced."""
+    g = load(golden_dir, f"g5_wrapped_{mode_name}.npz")
+    mode = {"sa": O.MODE_SA, "cma": O.MODE_CMA, "dma": O.MODE_DMA}[mode_name]
+    live = g["live_channels"]
+    T = g["dones"].shape[0]
+    n = g["state"].shape[2]
+    R = 3 if mode == O.MODE_DMA else 1
+    agents = 3 if mode == O.MODE_DMA else 1
+    prm = O.params(max_episode_length=int(g["max_len"]))
+    quat = np.isin(live, list(range(O.CH_RQZ, O.CH_RQZ + 12)))
+    u_off = np.concatenate([[0], np.cumsum(g["n_u"])])
+    z_off = np.concatenate([[0], np.cumsum(g["n_z"])])
+    for t in range(T):
+        if t == 0:
+            env = O.HostEnv(n)
+            env.state[:] = g["init_state"]
+            env.progress[:] = 0
+            env.reset[:] = 1
+            ou = np.zeros((n, 12), np.float32)
+        else:
+            env = _env_from_live(n, live, g["state"][t - 1], g["progress_f"][t - 1][::R].astype(np.int64),
+                                 g["dones"][t - 1][::R])
+            ou = g["action_buf"][t - 1].copy()
+        io = O.make_io(n, mode)
+        io["ou_buf"][:] = ou
+        draws, keep = O.make_draws(g["uniforms"][u_off[t]:u_off[t + 1]], g["normals"][z_off[t]:z_off[t + 1]])
+        O.step(env, mode, g["actions"][t], io, prm, draws)
+        assert draws.uniform_pos == g["n_u"][t] and draws.normal_pos == g["n_z"][t]
+        np.testing.assert_array_equal(io["ou_buf"], g["action_buf"][t], err_msg=f"step {t}")
+        if mode == O.MODE_DMA:
+            np.testing.assert_array_equal(io["dones_rep"], g["dones"][t])
+        else:
+            np.testing.assert_array_equal(env.reset, g["dones"][t])
+        np.testing.assert_array_equal(io["time_outs"], g["time_outs"][t])
+        np.testing.assert_array_equal(io["progress_f"], g["progress_f"][t])
+        np.testing.assert_allclose(io["rew"], g["rews"][t], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(io["reward_sum"], g["reward"][t], rtol=1e-6, atol=2e-6)
+        assert_obs_equal(io["obs"], g["obs"][t], agents=1)
+        assert_obs_equal(io["terminal_obs"], g["terminal_obs"][t], agents=1)
+        st = env.state[live]
+        np.testing.assert_array_equal(st[~quat], g["state"][t][~quat])
+        np.testing.assert_allclose(st[quat], g["state"][t][quat], atol=TRIG_ATOL, rtol=0)
+    assert g["dones"].sum() > 0
+    if mode == O.MODE_DMA:
+        assert int(g["num_envs"]) == 3 * n  # DMA re-assigns num_environments (envs/wrappers.py:154)

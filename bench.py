@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: the VSS match step (BASELINE.json north_star) on MI355X.
+
+One *step* = one `vss_step` launch advancing every field of this rank by one control step
+(dt = 0.05 s) under synthetic random actions, with the reference's full VecTask.step output
+contract (obs + terminal obs (N,2,3,52), rewards (N,2,3,4), dones, time-outs, progress) —
+BASELINE.json configs[1]/[2] at 65,536 fields per GPU.  Fields are independent, so ranks shard
+them with no data-path collective (weak scaling); the only collectives are the timing barrier
+and the max-over-ranks of the elapsed time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--fields F] [--mode full|sa|cma|dma]
+
+Rank 0 prints ONE JSON line (value = env-steps/s summed over all ranks = fields x ranks x K /
+max-over-ranks time).  `roofline.achieved` = algorithmic bytes per launch / mean launch time
+measured with HIP events on the launch stream; `cpu_baseline` = the C oracle (oracle/) on one
+host core over a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "rsoccer-isaac-cleanrl_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "env-steps/s (num_envs×horizon) at 65 536 envs; PPO wall-clock to 1e8 steps"
+HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip table (spec)
+
+# Algorithmic HBM bytes per field-step of each contract:
+#   state 46 live fp32 channels read+write (368), progress/reset int64 r+w (32), rng counter r+w (8)
+#   FULL: actions 48 + dof_velocity_buf write 48 + obs 1248 + terminal obs 1248 + rew 96
+#         + time_out 1 + progress_f 4                                           = 3101 B
+#   SA:   learner action 8 + OU buffer r+w 96 + dof 48 + obs 208 + terminal obs 208 + rew 16
+#         + reward 4 + time_out 1 + progress_f 4                                  = 1001 B
+BYTES = {
+    "full": 368 + 32 + 8 + 48 + 48 + 1248 + 1248 + 96 + 1 + 4,
+    "sa": 368 + 32 + 8 + 8 + 96 + 48 + 208 + 208 + 16 + 4 + 1 + 4,
+    "cma": 368 + 32 + 8 + 24 + 96 + 48 + 208 + 208 + 16 + 4 + 1 + 4,
+    "dma": 368 + 32 + 8 + 24 + 96 + 48 + 624 + 624 + 48 + 12 + 24 + 3 + 12,
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--fields", type=int, default=65536, help="fields (3v3 matches) per GPU")
+    p.add_argument("--mode", default="full", choices=["full", "sa", "cma", "dma"])
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(seconds: float):
+    """The C oracle (scalar, 1 core) on the same workload shape: 4,096 fields, random actions."""
+    import oracle as O
+    n = 4096
+    h = O.HostEnv(n)
+    prm = O.params(seed=1)
+    O.reset_dones(h, prm)
+    io = O.make_io(n, O.MODE_FULL)
+    gen = np.random.default_rng(1)
+    acts = [gen.uniform(-1, 1, (n, 12)).astype(np.float32) for _ in range(8)]
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        O.step(h, O.MODE_FULL, acts[steps % 8], io, prm)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": n * steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/vss_oracle.c FULL contract, {n} fields x {steps} steps ({el:.1f} s), "
+                      f"random actions, 1 thread, host CPU: {cpu_model()}"}
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+
+    from envs.vss import VSS, default_cfg
+    from envs import wrappers as Wr
+    from vss_amd import _native as N
+
+    n = args.fields
+    cfg = default_cfg(n)
+    cfg["env"]["seed"] = 1 + rank  # per-rank stream (seed + rank)
+    env = VSS(cfg, str(dev), str(dev), 0, True, False, False)
+    mode = {"full": N.MODE_FULL, "sa": N.MODE_SA, "cma": N.MODE_CMA, "dma": N.MODE_DMA}[args.mode]
+
+    # inputs resident in HBM before the timed region: a pool of random action batches
+    rows, width = {"full": (n, 12), "sa": (n, 2), "cma": (n, 6), "dma": (3 * n, 2)}[args.mode]
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    pool = [torch.rand((rows, width), device=dev, generator=gen) * 2 - 1 for _ in range(16)]
+    if mode == N.MODE_FULL:
+        io = dict(obs=env.obs_buf, terminal_obs=env.terminal_obs_buf, rew=env.rew_buf, reward_sum=None,
+                  time_outs=env.timeout_buf, progress_f=env.progress_f_buf)
+    else:
+        W = {"sa": Wr.SingleAgent, "cma": Wr.CMA, "dma": Wr.DMA}[args.mode](env)
+        io = dict(ou_buf=W.action_buf, obs=W._obs, terminal_obs=W._terminal_obs, rew=W._rews,
+                  reward_sum=W._reward, dones_rep=W._dones, time_outs=W._time_outs, progress_f=W._progress)
+
+    # pre-built ctypes arguments: the timed loop is launch-only (no per-step Python allocation)
+    lib = N.load()
+    stream = N.stream_of(dev)
+    prm, st = env._c_params(), env._c_state()
+    cios = [N.VssStepIO(a.data_ptr(), N.ptr(io.get("ou_buf")), N.ptr(io["obs"]), N.ptr(io["terminal_obs"]),
+                        N.ptr(io["rew"]), N.ptr(io.get("reward_sum")), N.ptr(io.get("dones_rep")),
+                        N.ptr(io["time_outs"]), N.ptr(io["progress_f"])) for a in pool]
+    byref = N.ctypes.byref
+
+    def launch(k):
+        rc = lib.vss_step(stream, n, mode, byref(prm), byref(st), byref(cios[k % len(cios)]))
+        if rc:
+            N.check(rc, "vss_step")
+
+    for k in range(args.warmup):
+        launch(k)
+    torch.cuda.synchronize()
+
+    # per-launch HIP events on the launch stream (torch's current stream) -> kernel time
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record()
+        launch(k)
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+
+    if rank == 0:
+        agents = 3 if args.mode == "dma" else 1
+        value = n * world * args.steps / elapsed
+        algo = BYTES[args.mode] * n
+        achieved = algo / (kern_ms * 1e-3)
+        traffic = None
+        tfile = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(tfile):
+            try:
+                tj = json.load(open(tfile))
+                if tj.get("fields") == n and tj.get("mode") == args.mode:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (uniform random actions in [-1,1], resident in HBM)",
+            "config": {"workload": f"vss_step {args.mode.upper()} contract: {n} fields/GPU, one launch per "
+                                   f"control step, random actions (BASELINE configs[1]/[2] shape)",
+                       "fields_per_gpu": n, "mode": args.mode, "agent_rows_per_field": agents,
+                       "parallelism": f"fields sharded over {world} GPU(s), no data-path collective"},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": algo, "kernel_ms": kern_ms},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,780 @@
+// vss_step.hip — MI355X (gfx950) kernels behind the C ABI of include/vss.h.
+//
+// One VSS field (a 3v3 match) per lane, 64 fields per wave / workgroup.  Per step a lane
+//   1. loads its field's 46 live fp32 state channels from the SoA state (coalesced, 256 B per
+//      wave-instruction per channel) plus progress/reset/rng counter,
+//   2. gathers its 12 actions (and, in SA/CMA/DMA mode, the OU action buffer) through an LDS
+//      transpose (16-B coalesced global loads of the wave's contiguous AoS block),
+//   3. runs the 2D physics for NSUB substeps in registers,
+//   4. computes rewards / dones (envs/vss.py:218-265, 578-655),
+//   5. writes the terminal observation, resets done fields (Philox rejection sampling,
+//      envs/vss.py:267-333), writes the observation — both observations through an LDS
+//      record (58 floats per field) that the wave streams out with 16-B coalesced stores in
+//      the (N, A, 52) layout, using a compile-time gather table (envs/vss.py:530-575),
+//   6. stores state, bookkeeping and the AoS reward block (LDS transpose again).
+// Everything is float32 with FMA contraction disabled (-ffp-contract=off and the pragma
+// below): results are bit-identical to the CPU oracle (oracle/vss_oracle.c).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/vss.h"
+
+#pragma clang fp contract(off)
+
+namespace vss {
+
+constexpr int kWave = 64;
+constexpr int kRec = 59;  // LDS floats per field record (58 used, odd stride: no bank conflicts)
+
+// ---- model constants (reference values cited in oracle/vss_oracle.c) --------
+constexpr int NSUB = 4;
+#define K_H 0.0125f
+#define K_HH 0.00625f
+#define K_FIELD_HX 0.75f
+#define K_FIELD_HY 0.65f
+#define K_GOAL_HY 0.2f
+#define K_GOAL_BACK_X 0.85f
+#define K_BALL_R 0.02134f
+#define K_BALL_R2 0.00045539559f
+#define K_ROBOT_HALF 0.035f
+#define K_ROBOT_R 0.04f
+#define K_RR_DIST 0.08f
+#define K_RR_DIST2 0.0064f
+#define K_WHEEL_RAD_S 42.0f
+#define K_WHEEL_R 0.024f
+#define K_HALF_TRACK 0.03375f
+#define K_INV_TRACK 14.814815f
+#define K_DV 0.075f
+#define K_DL 0.0858375f
+#define K_BALL_DAMP 0.998125f
+#define K_W_ROBOT_BR 0.09465021f
+#define K_W_BALL_BR 0.90534979f
+#define K_MIN_DIST 0.07f
+#define K_TWO_PI 6.2831855f
+#define K_PI 3.1415927f
+#define K_OU_THETA 0.1f
+#define K_OU_SIGMA 0.15f
+constexpr int kMaxRejectRounds = 64;
+constexpr uint32_t kPurposeOU = 1u, kPurposePos = 2u, kPurposeAng = 3u, kExternal = 0x80u;
+
+// ---- observation gather table ---------------------------------------------------------------
+// For float4 index j4 (0..77) of a field's (6, 52) observation block: 4 bytes, each
+// (source index into the 58-float LDS record) | 0x80 if the value is negated (yellow mirror).
+struct ObsTable {
+  uint32_t w[78];
+};
+
+constexpr ObsTable make_obs_table() {
+  ObsTable t{};
+  for (int j = 0; j < 312; ++j) {
+    int a = j / 52, e = j % 52, team = a / 3, idx = a % 3;
+    int src = 0;
+    bool neg = false;
+    if (e < 4) {
+      src = e;
+      neg = team == 1;
+    } else if (e < 31) {
+      int k = (e - 4) / 9, q = (e - 4) % 9;
+      int r = team * 3 + (idx + k) % 3;
+      src = 4 + r * 9 + q;
+      neg = team == 1 && q < 6;
+    } else {
+      int k = (e - 31) / 7, q = (e - 31) % 7;
+      int r = (1 - team) * 3 + k;
+      src = 4 + r * 9 + q;
+      neg = team == 1 && q < 6;
+    }
+    uint32_t byte = (uint32_t)src | (neg ? 0x80u : 0u);
+    t.w[j / 4] |= byte << (8 * (j % 4));
+  }
+  return t;
+}
+
+__constant__ ObsTable kObsTab = make_obs_table();
+
+// ---- math (transcendental-free; identical op sequence in oracle/vss_oracle.c) ----------------
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+__device__ __forceinline__ void philox(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t c2,
+                                       uint32_t c3, uint32_t out[4]) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * 5.9604645e-08f; }
+__device__ __forceinline__ float u01_open0(uint32_t x) { return (float)((x >> 8) + 1u) * 5.9604645e-08f; }
+
+__device__ __forceinline__ void sincos_poly(float r, float& s, float& c) {
+  float r2 = r * r;
+  s = r + r * r2 * (-0.16666667f + r2 * (0.008333334f + r2 * (-1.9841270e-4f + r2 * 2.7557319e-6f)));
+  c = 1.0f + r2 * (-0.5f + r2 * (0.041666668f + r2 * (-1.3888889e-3f + r2 * (2.4801587e-5f + r2 * (-2.7557319e-7f)))));
+}
+
+__device__ __forceinline__ void sincos_small(float x, float& s, float& c) {
+  int k = (int)(x * 0.63661977f + (x >= 0.0f ? 0.5f : -0.5f));
+  float kf = (float)k;
+  float r = (x - kf * 1.5707964f) - kf * (-4.3711390e-8f);
+  float sr, cr;
+  sincos_poly(r, sr, cr);
+  if (k == 0) { s = sr; c = cr; }
+  else if (k == 1) { s = cr; c = -sr; }
+  else if (k == -1) { s = -cr; c = sr; }
+  else { s = -sr; c = -cr; }
+}
+
+__device__ __forceinline__ void sincos_turn(float u, float& s, float& c) {
+  float v = u * 4.0f;
+  int q = (int)v;
+  float t = v - (float)q;
+  float r = (t - 0.5f) * 1.5707964f;
+  float sr, cr;
+  sincos_poly(r, sr, cr);
+  float cp = (cr - sr) * 0.70710677f;
+  float sp = (cr + sr) * 0.70710677f;
+  if (q == 0) { c = cp; s = sp; }
+  else if (q == 1) { c = -sp; s = cp; }
+  else if (q == 2) { c = -cp; s = -sp; }
+  else { c = sp; s = -cp; }
+}
+
+__device__ __forceinline__ float logf_poly(float x) {
+  uint32_t u = __float_as_uint(x);
+  int e = (int)((u >> 23) & 0xffu) - 127;
+  float m = __uint_as_float((u & 0x7fffffu) | 0x3f800000u);
+  if (m > 1.4142135f) { m = m * 0.5f; e = e + 1; }
+  float s = (m - 1.0f) / (m + 1.0f);
+  float s2 = s * s;
+  float p = 2.0f + s2 * (0.6666667f + s2 * (0.4f + s2 * (0.2857143f + s2 * (0.22222222f + s2 * 0.18181819f))));
+  return (float)e * 0.69314718f + s * p;
+}
+
+// ---- per-field body state in registers ---------------------------------------------------------
+struct Bodies {
+  float bx, by, bvx, bvy;
+  float x[6], y[6], qz[6], qw[6], vx[6], vy[6], w[6];
+  float c[6], s[6];
+};
+
+__device__ __forceinline__ void heading(Bodies& b, int i) {
+  b.c[i] = b.qw[i] * b.qw[i] - b.qz[i] * b.qz[i];
+  b.s[i] = 2.0f * b.qw[i] * b.qz[i];
+}
+
+__device__ __forceinline__ void contact_robot_robot(Bodies& b, int i, int j) {
+  float dx = b.x[j] - b.x[i], dy = b.y[j] - b.y[i];
+  float d2 = dx * dx + dy * dy;
+  if (d2 < K_RR_DIST2) {
+    float d = sqrtf(d2);
+    float nx = 1.0f, ny = 0.0f;
+    if (d > 1e-9f) { nx = dx / d; ny = dy / d; }
+    float half = (K_RR_DIST - d) * 0.5f;
+    b.x[i] = b.x[i] - nx * half; b.y[i] = b.y[i] - ny * half;
+    b.x[j] = b.x[j] + nx * half; b.y[j] = b.y[j] + ny * half;
+    float vn = (b.vx[j] - b.vx[i]) * nx + (b.vy[j] - b.vy[i]) * ny;
+    if (vn < 0.0f) {
+      float jn = vn * 0.5f;
+      b.vx[i] = b.vx[i] + nx * jn; b.vy[i] = b.vy[i] + ny * jn;
+      b.vx[j] = b.vx[j] - nx * jn; b.vy[j] = b.vy[j] - ny * jn;
+    }
+  }
+}
+
+__device__ __forceinline__ void contact_ball_robot(Bodies& b, int i) {
+  float dx = b.bx - b.x[i], dy = b.by - b.y[i];
+  float c = b.c[i], s = b.s[i];
+  float lx = c * dx + s * dy;
+  float ly = c * dy - s * dx;
+  float cx = clampf(lx, -K_ROBOT_HALF, K_ROBOT_HALF);
+  float cy = clampf(ly, -K_ROBOT_HALF, K_ROBOT_HALF);
+  float ex = lx - cx, ey = ly - cy;
+  float d2 = ex * ex + ey * ey;
+  float nlx, nly, pen;
+  bool hit;
+  if (d2 > 0.0f) {
+    hit = d2 < K_BALL_R2;
+    float d = sqrtf(d2);
+    nlx = ex / d; nly = ey / d;
+    pen = K_BALL_R - d;
+  } else {
+    hit = true;
+    float px = K_ROBOT_HALF - fabsf(lx), py = K_ROBOT_HALF - fabsf(ly);
+    if (px < py) { nlx = lx >= 0.0f ? 1.0f : -1.0f; nly = 0.0f; pen = px + K_BALL_R; }
+    else { nlx = 0.0f; nly = ly >= 0.0f ? 1.0f : -1.0f; pen = py + K_BALL_R; }
+  }
+  if (hit) {
+    float nx = c * nlx - s * nly;
+    float ny = s * nlx + c * nly;
+    float pr = pen * K_W_ROBOT_BR, pb = pen * K_W_BALL_BR;
+    b.x[i] = b.x[i] - nx * pr; b.y[i] = b.y[i] - ny * pr;
+    b.bx = b.bx + nx * pb; b.by = b.by + ny * pb;
+    float vn = (b.bvx - b.vx[i]) * nx + (b.bvy - b.vy[i]) * ny;
+    if (vn < 0.0f) {
+      float jr = vn * K_W_ROBOT_BR, jb = vn * K_W_BALL_BR;
+      b.vx[i] = b.vx[i] + nx * jr; b.vy[i] = b.vy[i] + ny * jr;
+      b.bvx = b.bvx - nx * jb; b.bvy = b.bvy - ny * jb;
+    }
+  }
+}
+
+// Disc of radius r against the field walls (envs/vss.py:449-518), folded into x, y >= 0.
+__device__ __forceinline__ void contact_walls(float& x, float& y, float& vx, float& vy, float r) {
+  float sx = x < 0.0f ? -1.0f : 1.0f, sy = y < 0.0f ? -1.0f : 1.0f;
+  float ax = fabsf(x), ay = fabsf(y);
+  float avx = vx * sx, avy = vy * sy;
+  if (ax <= K_FIELD_HX) {
+    if (ay <= K_GOAL_HY) {
+      float dx = ax - K_FIELD_HX, dy = ay - K_GOAL_HY;
+      float d2 = dx * dx + dy * dy;
+      if (d2 < r * r) {
+        float d = sqrtf(d2);
+        float nx = -1.0f, ny = 0.0f;
+        if (d > 1e-9f) { nx = dx / d; ny = dy / d; }
+        float pen = r - d;
+        ax = ax + nx * pen; ay = ay + ny * pen;
+        float vn = avx * nx + avy * ny;
+        if (vn < 0.0f) { avx = avx - nx * vn; avy = avy - ny * vn; }
+      }
+    } else {
+      float pen = ax + r - K_FIELD_HX;
+      if (pen > 0.0f) { ax = ax - pen; if (avx > 0.0f) avx = 0.0f; }
+    }
+  } else {
+    if (ay <= K_GOAL_HY) {
+      float pen = ay + r - K_GOAL_HY;
+      if (pen > 0.0f) { ay = ay - pen; if (avy > 0.0f) avy = 0.0f; }
+    } else {
+      float px = ax - K_FIELD_HX + r, py = ay - K_GOAL_HY + r;
+      if (px < py) { ax = ax - px; if (avx > 0.0f) avx = 0.0f; }
+      else { ay = ay - py; if (avy > 0.0f) avy = 0.0f; }
+    }
+  }
+  { float pen = ay + r - K_FIELD_HY; if (pen > 0.0f) { ay = ay - pen; if (avy > 0.0f) avy = 0.0f; } }
+  { float pen = ax + r - K_GOAL_BACK_X; if (pen > 0.0f) { ax = ax - pen; if (avx > 0.0f) avx = 0.0f; } }
+  x = ax * sx; y = ay * sy; vx = avx * sx; vy = avy * sy;
+}
+
+__device__ __forceinline__ void physics(Bodies& b, const float a[12]) {
+  float tl[6], tr[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    tl[i] = (a[2 * i] * K_WHEEL_RAD_S) * K_WHEEL_R;
+    tr[i] = (a[2 * i + 1] * K_WHEEL_RAD_S) * K_WHEEL_R;
+    heading(b, i);
+  }
+#pragma unroll 1
+  for (int sub = 0; sub < NSUB; ++sub) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      float c = b.c[i], s = b.s[i];
+      float vf = c * b.vx[i] + s * b.vy[i];
+      float vl = c * b.vy[i] - s * b.vx[i];
+      float wl = vf - b.w[i] * K_HALF_TRACK;
+      float wr = vf + b.w[i] * K_HALF_TRACK;
+      wl = wl + clampf(tl[i] - wl, -K_DV, K_DV);
+      wr = wr + clampf(tr[i] - wr, -K_DV, K_DV);
+      vf = (wl + wr) * 0.5f;
+      b.w[i] = (wr - wl) * K_INV_TRACK;
+      vl = vl - clampf(vl, -K_DL, K_DL);
+      b.vx[i] = c * vf - s * vl;
+      b.vy[i] = s * vf + c * vl;
+    }
+    b.bvx = b.bvx * K_BALL_DAMP;
+    b.bvy = b.bvy * K_BALL_DAMP;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      b.x[i] = b.x[i] + b.vx[i] * K_H;
+      b.y[i] = b.y[i] + b.vy[i] * K_H;
+      float sh, ch;
+      sincos_small(b.w[i] * K_HH, sh, ch);
+      float qz = b.qz[i] * ch + b.qw[i] * sh;
+      float qw = b.qw[i] * ch - b.qz[i] * sh;
+      float nrm = sqrtf(qz * qz + qw * qw);
+      b.qz[i] = qz / nrm;
+      b.qw[i] = qw / nrm;
+      heading(b, i);
+    }
+    b.bx = b.bx + b.bvx * K_H;
+    b.by = b.by + b.bvy * K_H;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = i + 1; j < 6; ++j) contact_robot_robot(b, i, j);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) contact_ball_robot(b, i);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) contact_walls(b.x[i], b.y[i], b.vx[i], b.vy[i], K_ROBOT_R);
+    contact_walls(b.bx, b.by, b.bvx, b.bvy, K_BALL_R);
+  }
+}
+
+// ---- state I/O -----------------------------------------------------------------------------------
+__device__ __forceinline__ void load_bodies(const float* __restrict__ st, int64_t n, int64_t f, Bodies& b) {
+  b.bx = st[VSS_CH_BALL_X * n + f]; b.by = st[VSS_CH_BALL_Y * n + f];
+  b.bvx = st[VSS_CH_BALL_VX * n + f]; b.bvy = st[VSS_CH_BALL_VY * n + f];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    b.x[i] = st[(VSS_CH_RX + i) * n + f]; b.y[i] = st[(VSS_CH_RY + i) * n + f];
+    b.qz[i] = st[(VSS_CH_RQZ + i) * n + f]; b.qw[i] = st[(VSS_CH_RQW + i) * n + f];
+    b.vx[i] = st[(VSS_CH_RVX + i) * n + f]; b.vy[i] = st[(VSS_CH_RVY + i) * n + f];
+    b.w[i] = st[(VSS_CH_RW + i) * n + f];
+  }
+}
+
+__device__ __forceinline__ void store_bodies(float* __restrict__ st, int64_t n, int64_t f, const Bodies& b) {
+  st[VSS_CH_BALL_X * n + f] = b.bx; st[VSS_CH_BALL_Y * n + f] = b.by;
+  st[VSS_CH_BALL_VX * n + f] = b.bvx; st[VSS_CH_BALL_VY * n + f] = b.bvy;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    st[(VSS_CH_RX + i) * n + f] = b.x[i]; st[(VSS_CH_RY + i) * n + f] = b.y[i];
+    st[(VSS_CH_RQZ + i) * n + f] = b.qz[i]; st[(VSS_CH_RQW + i) * n + f] = b.qw[i];
+    st[(VSS_CH_RVX + i) * n + f] = b.vx[i]; st[(VSS_CH_RVY + i) * n + f] = b.vy[i];
+    st[(VSS_CH_RW + i) * n + f] = b.w[i];
+  }
+}
+
+// ---- wave-cooperative AoS <-> per-lane transposes through LDS -----------------------------------
+// A wave owns fields [f0, f0 + nv); their W-float records are contiguous in global memory.
+template <int W>
+__device__ __forceinline__ void coop_load(const float* __restrict__ g, int nv, float* lds, int lane) {
+  const int total = nv * W;
+  if constexpr (W % 4 == 0) {
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    for (int q = lane; q < total / 4; q += kWave) {
+      float4 v = g4[q];
+      int e = q * 4, fl = e / W, k = e - fl * W;
+      float* d = lds + fl * kRec + k;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+  } else {
+    const float2* g2 = reinterpret_cast<const float2*>(g);
+    for (int q = lane; q < total / 2; q += kWave) {
+      float2 v = g2[q];
+      int e = q * 2, fl = e / W, k = e - fl * W;
+      float* d = lds + fl * kRec + k;
+      d[0] = v.x; d[1] = v.y;
+    }
+  }
+}
+
+template <int W>
+__device__ __forceinline__ void coop_store(float* __restrict__ g, int nv, const float* lds, int lane) {
+  const int total = nv * W;
+  if constexpr (W % 4 == 0) {
+    float4* g4 = reinterpret_cast<float4*>(g);
+    for (int q = lane; q < total / 4; q += kWave) {
+      int e = q * 4, fl = e / W, k = e - fl * W;
+      const float* s = lds + fl * kRec + k;
+      g4[q] = make_float4(s[0], s[1], s[2], s[3]);
+    }
+  } else {
+    float2* g2 = reinterpret_cast<float2*>(g);
+    for (int q = lane; q < total / 2; q += kWave) {
+      int e = q * 2, fl = e / W, k = e - fl * W;
+      const float* s = lds + fl * kRec + k;
+      g2[q] = make_float2(s[0], s[1]);
+    }
+  }
+}
+
+// Observation record of one field into LDS: ball (4) + 6 x (x, y, vx, vy, cos, sin, w, aL, aR).
+__device__ __forceinline__ void write_obs_record(float* rec, const Bodies& b, const float dof[12]) {
+  rec[0] = b.bx; rec[1] = b.by; rec[2] = b.bvx; rec[3] = b.bvy;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    float* o = rec + 4 + 9 * r;
+    o[0] = b.x[r]; o[1] = b.y[r]; o[2] = b.vx[r]; o[3] = b.vy[r];
+    o[4] = b.qw[r] * b.qw[r] - b.qz[r] * b.qz[r];
+    o[5] = 2.0f * b.qw[r] * b.qz[r];
+    o[6] = b.w[r]; o[7] = dof[2 * r]; o[8] = dof[2 * r + 1];
+  }
+}
+
+// Stream the wave's observation block (nv fields x A agents x 52) out of the LDS records.
+template <int A>
+__device__ __forceinline__ void coop_store_obs(float* __restrict__ out, int nv, const float* lds, int lane) {
+  constexpr int Q = 13 * A;  // float4 per field
+  const int total = nv * Q;
+  float4* o4 = reinterpret_cast<float4*>(out);
+  for (int q = lane; q < total; q += kWave) {
+    int fl = q / Q, j4 = q - fl * Q;
+    uint32_t t = kObsTab.w[j4];
+    const float* rec = lds + fl * kRec;
+    float4 v;
+    v.x = __uint_as_float(__float_as_uint(rec[t & 0x7fu]) ^ ((t & 0x80u) << 24));
+    v.y = __uint_as_float(__float_as_uint(rec[(t >> 8) & 0x7fu]) ^ ((t & 0x8000u) << 16));
+    v.z = __uint_as_float(__float_as_uint(rec[(t >> 16) & 0x7fu]) ^ ((t & 0x800000u) << 8));
+    v.w = __uint_as_float(__float_as_uint(rec[(t >> 24) & 0x7fu]) ^ (t & 0x80000000u));
+    o4[q] = v;
+  }
+}
+
+// ---- reset sampling (envs/vss.py:267-333), Philox counter (field, ctr, purpose<<24|round, blk) --
+__device__ __forceinline__ void reset_field(Bodies& b, uint32_t k0, uint32_t k1, uint32_t field, uint32_t ctr,
+                                            uint32_t ext) {
+  const float scale_x = 1.5f - 0.14f, scale_y = 1.3f - 0.14f;
+  float px[7], py[7];
+  for (uint32_t round = 0;; ++round) {
+    uint32_t o[16];
+#pragma unroll
+    for (int blk = 0; blk < 4; ++blk)
+      philox(k0, k1, field, ctr, ((kPurposePos | ext) << 24) | round, (uint32_t)blk, o + 4 * blk);
+#pragma unroll
+    for (int e = 0; e < 7; ++e) {
+      px[e] = (u01(o[2 * e]) - 0.5f) * scale_x;
+      py[e] = (u01(o[2 * e + 1]) - 0.5f) * scale_y;
+    }
+    bool close = false;
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+#pragma unroll
+      for (int j = i + 1; j < 7; ++j) {
+        float dx = px[i] - px[j], dy = py[i] - py[j];
+        close |= sqrtf(dx * dx + dy * dy) < K_MIN_DIST;
+      }
+    if (!close || round + 1 >= (uint32_t)kMaxRejectRounds) break;
+  }
+  b.bx = px[0]; b.by = py[0];
+  uint32_t o[8];
+  philox(k0, k1, field, ctr, ((kPurposeAng | ext) << 24), 0u, o);
+  philox(k0, k1, field, ctr, ((kPurposeAng | ext) << 24), 1u, o + 4);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    b.x[r] = px[1 + r]; b.y[r] = py[1 + r];
+    b.vx[r] = 0.0f; b.vy[r] = 0.0f; b.w[r] = 0.0f;
+    float ang = K_TWO_PI * u01(o[r]) + (-K_PI);
+    float sh, ch;
+    sincos_small(ang * 0.5f, sh, ch);
+    float nrm = sqrtf(sh * sh + ch * ch);
+    b.qz[r] = sh / nrm;
+    b.qw[r] = ch / nrm;
+  }
+  b.bvx = u01(o[6]) - 0.5f;
+  b.bvy = u01(o[7]) - 0.5f;
+}
+
+// ---- the step kernel -------------------------------------------------------------------------------
+struct StepArgs {
+  int64_t n;
+  vss_params p;
+  vss_state s;
+  vss_step_io io;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
+  constexpr int A = MODE == VSS_MODE_FULL ? 6 : (MODE == VSS_MODE_DMA ? 3 : 1);
+  constexpr int R = MODE == VSS_MODE_DMA ? 3 : 1;
+  constexpr int NL = MODE == VSS_MODE_SA ? 2 : 6;  // learner action floats per field
+  __shared__ float lds[kWave * kRec];
+
+  const int64_t n = args.n;
+  const int lane = threadIdx.x;
+  const int64_t f0 = (int64_t)blockIdx.x * kWave;
+  const int nv = (int)(n - f0 < kWave ? n - f0 : kWave);
+  const int64_t f = f0 + lane;
+  const bool valid = lane < nv;
+  const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
+  float* rec = lds + lane * kRec;
+
+  // -- actions: FULL reads (N,12); wrapped modes read + update the OU action buffer --------------
+  float a[12];
+  if constexpr (MODE == VSS_MODE_FULL) {
+    coop_load<12>(args.io.actions + f0 * 12, nv, lds, lane);
+  } else {
+    coop_load<12>(args.io.ou_buf + f0 * 12, nv, lds, lane);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 12; ++k) a[k] = rec[k];
+  __syncthreads();
+
+  int64_t progress = 0, reset_prev = 0;
+  uint32_t ctr = 0;
+  Bodies b = {};
+  if (valid) {
+    progress = args.s.progress_buf[f];
+    reset_prev = args.s.reset_buf[f];
+    ctr = args.s.rng_counter[f];
+    load_bodies(args.s.state, n, f, b);
+  }
+
+  if constexpr (MODE != VSS_MODE_FULL) {
+    // random_ou (envs/wrappers.py:5-19): a <- clamp(a - 0.1 a + N(0, 0.15^2), -1, 1); the learner
+    // slots (pairs 0 for SA, 0..2 for CMA/DMA) are overwritten, so their normals are not needed.
+    constexpr int first_block = MODE == VSS_MODE_SA ? 0 : 1;
+#pragma unroll
+    for (int blk = first_block; blk < 3; ++blk) {
+      uint32_t o[4];
+      philox(k0, k1, (uint32_t)f, ctr, kPurposeOU << 24, (uint32_t)blk, o);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        int k = 4 * blk + 2 * h;
+        if (k < NL) continue;
+        float u1 = u01_open0(o[2 * h]);
+        float u2 = u01(o[2 * h + 1]);
+        float rad = sqrtf(-2.0f * logf_poly(u1));
+        float sz, cz;
+        sincos_turn(u2, sz, cz);
+        a[k] = clampf((a[k] - K_OU_THETA * a[k]) + K_OU_SIGMA * (rad * cz), -1.0f, 1.0f);
+        a[k + 1] = clampf((a[k + 1] - K_OU_THETA * a[k + 1]) + K_OU_SIGMA * (rad * sz), -1.0f, 1.0f);
+      }
+    }
+    coop_load<NL>(args.io.actions + f0 * NL, nv, lds, lane);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NL; ++k) a[k] = rec[k];
+    __syncthreads();
+  }
+  float ou[12];
+  if constexpr (MODE != VSS_MODE_FULL) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) ou[k] = a[k];
+  }
+
+  // -- Ext VecTask.step clamp + pre_physics_step (envs/vss.py:180-187) -----------------------------
+  const float clip = args.p.clip_actions;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) a[k] = clampf(a[k], -clip, clip);
+  if (reset_prev != 0) progress = 0;
+
+  float pbx = b.bx, pby = b.by, prx[6], pry[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) { prx[i] = b.x[i]; pry[i] = b.y[i]; }
+
+  // -- gym.simulate replacement ------------------------------------------------------------------------
+  if (valid) physics(b, a);
+
+  // -- post_physics_step: progress, rewards, dones (envs/vss.py:189-265) ----------------------------------
+  progress += 1;
+  const float bx = b.bx, by = b.by;
+  const bool is_goal = (fabsf(bx) > K_FIELD_HX) && (fabsf(by) < K_GOAL_HY);
+  const float g = is_goal ? (bx > 0.0f ? 1.0f : (bx < 0.0f ? -1.0f : 0.0f)) : 0.0f;
+  float grad;
+  {
+    float lx = bx - (-K_FIELD_HX), ly = by - (-0.0f), rx = bx - K_FIELD_HX, ry = by - 0.0f;
+    float pot = sqrtf(lx * lx + ly * ly) - sqrtf(rx * rx + ry * ry);
+    float plx = pbx - (-K_FIELD_HX), ply = pby - (-0.0f), prx_ = pbx - K_FIELD_HX, pry_ = pby - 0.0f;
+    float ppot = sqrtf(plx * plx + ply * ply) - sqrtf(prx_ * prx_ + pry_ * pry_);
+    grad = pot - ppot;
+  }
+  float rew[24];
+#pragma unroll
+  for (int ag = 0; ag < 6; ++ag) {
+    const bool blue = ag < 3;
+    float r0 = 0.0f, r1 = 0.0f, r2 = 0.0f, r3 = 0.0f;
+    if (args.p.w_goal > 0.0f) r0 = (blue ? g : (0.0f - g)) * args.p.w_goal;
+    if (args.p.w_grad > 0.0f) r1 = (blue ? grad : -grad) * args.p.w_grad;
+    if (args.p.w_move > 0.0f) {
+      float dx0 = prx[ag] - pbx, dy0 = pry[ag] - pby;
+      float dx1 = b.x[ag] - bx, dy1 = b.y[ag] - by;
+      float pd = sqrtf(dx0 * dx0 + dy0 * dy0), d = sqrtf(dx1 * dx1 + dy1 * dy1);
+      r2 = 0.0f + (pd - d) * args.p.w_move;
+    }
+    if (args.p.w_energy > 0.0f)
+      r3 = 0.0f + (-((fabsf(a[2 * ag]) + fabsf(a[2 * ag + 1])) / 2.0f)) * args.p.w_energy;
+    rew[4 * ag] = r0; rew[4 * ag + 1] = r1; rew[4 * ag + 2] = r2; rew[4 * ag + 3] = r3;
+  }
+  const int64_t done = (is_goal || progress >= (int64_t)args.p.max_episode_length) ? 1 : 0;
+
+  // -- terminal observation (envs/vss.py:195-196) ----------------------------------------------------------
+  write_obs_record(rec, b, a);
+  __syncthreads();
+  coop_store_obs<A>(args.io.terminal_obs + f0 * (52 * A), nv, lds, lane);
+  __syncthreads();
+
+  // -- reset_dones (envs/vss.py:202, 267-333) ---------------------------------------------------------------
+  float dof[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) dof[k] = a[k];
+  if (valid && done) {
+    reset_field(b, k0, k1, (uint32_t)f, ctr, 0u);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) dof[k] = dof[k] * 0.0f;
+  }
+
+  // -- observation after reset (envs/vss.py:203) -------------------------------------------------------------
+  write_obs_record(rec, b, dof);
+  __syncthreads();
+  coop_store_obs<A>(args.io.obs + f0 * (52 * A), nv, lds, lane);
+  __syncthreads();
+
+  // -- bookkeeping --------------------------------------------------------------------------------------------
+  const uint8_t time_out = (progress >= (int64_t)args.p.max_episode_length - 1) && done != 0;
+  if (valid) {
+    store_bodies(args.s.state, n, f, b);
+    args.s.progress_buf[f] = progress;
+    args.s.reset_buf[f] = done;
+    args.s.rng_counter[f] = ctr + 1u;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      args.io.time_outs[f * R + k] = time_out;
+      args.io.progress_f[f * R + k] = (float)progress;
+    }
+    if constexpr (MODE == VSS_MODE_DMA) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) args.io.dones_rep[f * 3 + k] = done;
+    }
+  }
+
+  // dof_velocity_buf (N,12) and, wrapped, the OU action buffer (zeroed for done fields)
+#pragma unroll
+  for (int k = 0; k < 12; ++k) rec[k] = dof[k];
+  __syncthreads();
+  coop_store<12>(args.s.dof_velocity_buf + f0 * 12, nv, lds, lane);
+  __syncthreads();
+  if constexpr (MODE != VSS_MODE_FULL) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) rec[k] = done ? ou[k] * 0.0f : ou[k];
+    __syncthreads();
+    coop_store<12>(args.io.ou_buf + f0 * 12, nv, lds, lane);
+    __syncthreads();
+  }
+
+  // rewards
+  if constexpr (MODE == VSS_MODE_FULL) {
+#pragma unroll
+    for (int k = 0; k < 24; ++k) rec[k] = rew[k];
+    __syncthreads();
+    coop_store<24>(args.io.rew + f0 * 24, nv, lds, lane);
+    if (valid && args.io.reward_sum) args.io.reward_sum[f] = ((rew[0] + rew[1]) + rew[2]) + rew[3];
+  } else if constexpr (MODE == VSS_MODE_SA) {
+    if (valid) {
+      reinterpret_cast<float4*>(args.io.rew)[f] = make_float4(rew[0], rew[1], rew[2], rew[3]);
+      args.io.reward_sum[f] = ((rew[0] + rew[1]) + rew[2]) + rew[3];
+    }
+  } else if constexpr (MODE == VSS_MODE_CMA) {
+    if (valid) {
+      float m[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) m[c] = ((rew[c] + rew[4 + c]) + rew[8 + c]) / 3.0f;
+      reinterpret_cast<float4*>(args.io.rew)[f] = make_float4(m[0], m[1], m[2], m[3]);
+      args.io.reward_sum[f] = ((m[0] + m[1]) + m[2]) + m[3];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) rec[k] = rew[k];
+    __syncthreads();
+    coop_store<12>(args.io.rew + f0 * 12, nv, lds, lane);
+    if (valid) {
+#pragma unroll
+      for (int ag = 0; ag < 3; ++ag)
+        args.io.reward_sum[f * 3 + ag] = ((rew[4 * ag] + rew[4 * ag + 1]) + rew[4 * ag + 2]) + rew[4 * ag + 3];
+    }
+  }
+}
+
+// External reset_dones: fields with reset_buf != 0 are re-sampled with the EXTERNAL purpose bit
+// and their rng counter advances (so repeated calls draw afresh).  dof_velocity_buf zeroed.
+__global__ __launch_bounds__(kWave) void reset_kernel(int64_t n, vss_params p, vss_state s) {
+  const int64_t f = (int64_t)blockIdx.x * kWave + threadIdx.x;
+  if (f >= n || s.reset_buf[f] == 0) return;
+  Bodies b;
+  load_bodies(s.state, n, f, b);
+  const uint32_t ctr = s.rng_counter[f];
+  reset_field(b, (uint32_t)p.seed, (uint32_t)(p.seed >> 32), (uint32_t)f, ctr, kExternal);
+  store_bodies(s.state, n, f, b);
+  s.rng_counter[f] = ctr + 1u;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) s.dof_velocity_buf[f * 12 + k] = s.dof_velocity_buf[f * 12 + k] * 0.0f;
+}
+
+template <int A>
+__global__ __launch_bounds__(kWave) void observe_kernel(int64_t n, vss_state s, float* obs) {
+  __shared__ float lds[kWave * kRec];
+  const int lane = threadIdx.x;
+  const int64_t f0 = (int64_t)blockIdx.x * kWave;
+  const int nv = (int)(n - f0 < kWave ? n - f0 : kWave);
+  const int64_t f = f0 + lane;
+  float* rec = lds + lane * kRec;
+  coop_load<12>(s.dof_velocity_buf + f0 * 12, nv, lds, lane);
+  __syncthreads();
+  float dof[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) dof[k] = rec[k];
+  __syncthreads();
+  Bodies b = {};
+  if (lane < nv) {
+    load_bodies(s.state, n, f, b);
+    write_obs_record(rec, b, dof);
+  }
+  __syncthreads();
+  coop_store_obs<A>(obs + f0 * (52 * A), nv, lds, lane);
+}
+
+}  // namespace vss
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+int vss_abi_version(void) { return VSS_ABI_VERSION; }
+
+const char* vss_error_string(int code) {
+  switch (code) {
+    case VSS_OK: return "ok";
+    case VSS_E_ARG: return "invalid argument (null buffer, bad size or bad mode)";
+    case VSS_E_LAUNCH: return "kernel launch failed";
+    default: return "unknown error";
+  }
+}
+
+static int check_state(int64_t n, const vss_state* st) {
+  if (n < 0 || n > (int64_t(1) << 26) || !st) return VSS_E_ARG;
+  if (!st->state || !st->progress_buf || !st->reset_buf || !st->dof_velocity_buf || !st->rng_counter)
+    return VSS_E_ARG;
+  return VSS_OK;
+}
+
+static int launch_status() { return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH; }
+
+int vss_step(void* stream, int64_t n, int32_t mode, const vss_params* p, const vss_state* st,
+             const vss_step_io* io) {
+  if (int rc = check_state(n, st)) return rc;
+  if (!p || !io || mode < VSS_MODE_FULL || mode > VSS_MODE_DMA) return VSS_E_ARG;
+  if (!io->actions || !io->obs || !io->terminal_obs || !io->rew || !io->time_outs || !io->progress_f)
+    return VSS_E_ARG;
+  if (mode != VSS_MODE_FULL && (!io->ou_buf || !io->reward_sum)) return VSS_E_ARG;
+  if (mode == VSS_MODE_DMA && !io->dones_rep) return VSS_E_ARG;
+  if (n == 0) return VSS_OK;
+  vss::StepArgs args{n, *p, *st, *io};
+  const dim3 grid((unsigned)((n + vss::kWave - 1) / vss::kWave)), block(vss::kWave);
+  hipStream_t s = (hipStream_t)stream;
+  switch (mode) {
+    case VSS_MODE_FULL: hipLaunchKernelGGL(vss::step_kernel<VSS_MODE_FULL>, grid, block, 0, s, args); break;
+    case VSS_MODE_SA: hipLaunchKernelGGL(vss::step_kernel<VSS_MODE_SA>, grid, block, 0, s, args); break;
+    case VSS_MODE_CMA: hipLaunchKernelGGL(vss::step_kernel<VSS_MODE_CMA>, grid, block, 0, s, args); break;
+    default: hipLaunchKernelGGL(vss::step_kernel<VSS_MODE_DMA>, grid, block, 0, s, args); break;
+  }
+  return launch_status();
+}
+
+int vss_reset_dones(void* stream, int64_t n, const vss_params* p, const vss_state* st) {
+  if (int rc = check_state(n, st)) return rc;
+  if (!p) return VSS_E_ARG;
+  if (n == 0) return VSS_OK;
+  const dim3 grid((unsigned)((n + vss::kWave - 1) / vss::kWave)), block(vss::kWave);
+  hipLaunchKernelGGL(vss::reset_kernel, grid, block, 0, (hipStream_t)stream, n, *p, *st);
+  return launch_status();
+}
+
+int vss_compute_observations(void* stream, int64_t n, const vss_state* st, float* obs, int32_t n_agents) {
+  if (int rc = check_state(n, st)) return rc;
+  if (!obs || !(n_agents == 1 || n_agents == 3 || n_agents == 6)) return VSS_E_ARG;
+  if (n == 0) return VSS_OK;
+  const dim3 grid((unsigned)((n + vss::kWave - 1) / vss::kWave)), block(vss::kWave);
+  hipStream_t s = (hipStream_t)stream;
+  if (n_agents == 6) hipLaunchKernelGGL(vss::observe_kernel<6>, grid, block, 0, s, n, *st, obs);
+  else if (n_agents == 3) hipLaunchKernelGGL(vss::observe_kernel<3>, grid, block, 0, s, n, *st, obs);
+  else hipLaunchKernelGGL(vss::observe_kernel<1>, grid, block, 0, s, n, *st, obs);
+  return launch_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,108 @@
+"""ctypes binding of libvss_amd.so — the C ABI declared in include/vss.h.
+
+The shared library is built in-tree by `make -C rsoccer-isaac-cleanrl_amd/csrc` (or
+`__graft_entry__.build()`).  There is no fallback: if the library is missing, or the device is
+not a ROCm GPU, the calls raise.  torch is imported first so that the HIP runtime the library
+links against (libamdhip64.so.7) is the one torch already loaded — one runtime, one set of
+streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads torch's HIP runtime before the library resolves it)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libvss_amd.so")
+CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "vss.h")
+
+ABI_VERSION = 1
+MODE_FULL, MODE_SA, MODE_CMA, MODE_DMA = 0, 1, 2, 3
+STATE_CHANNELS = 58
+CH_BALL_X, CH_BALL_Y, CH_BALL_VX, CH_BALL_VY = 0, 1, 2, 3
+CH_RX, CH_RY, CH_RQX, CH_RQY, CH_RQZ, CH_RQW, CH_RVX, CH_RVY, CH_RW = 4, 10, 16, 22, 28, 34, 40, 46, 52
+EXPORTED = ("vss_abi_version", "vss_error_string", "vss_step", "vss_reset_dones",
+            "vss_compute_observations")
+
+
+class VssParams(ctypes.Structure):
+    _fields_ = [
+        ("w_goal", ctypes.c_float),
+        ("w_grad", ctypes.c_float),
+        ("w_move", ctypes.c_float),
+        ("w_energy", ctypes.c_float),
+        ("clip_actions", ctypes.c_float),
+        ("max_episode_length", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class VssState(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in
+                ("state", "progress_buf", "reset_buf", "dof_velocity_buf", "rng_counter")]
+
+
+class VssStepIO(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in
+                ("actions", "ou_buf", "obs", "terminal_obs", "rew", "reward_sum", "dones_rep",
+                 "time_outs", "progress_f")]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libvss_amd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(
+            f"VSS HIP library not found at {LIB_PATH}; build it with "
+            f"`make -C {CSRC}` or `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    P, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+    L.vss_abi_version.restype = ctypes.c_int
+    L.vss_error_string.argtypes = [ctypes.c_int]
+    L.vss_error_string.restype = ctypes.c_char_p
+    L.vss_step.argtypes = [P, i64, i32, P, P, P]
+    L.vss_step.restype = ctypes.c_int
+    L.vss_reset_dones.argtypes = [P, i64, P, P]
+    L.vss_reset_dones.restype = ctypes.c_int
+    L.vss_compute_observations.argtypes = [P, i64, P, P, i32]
+    L.vss_compute_observations.restype = ctypes.c_int
+    if L.vss_abi_version() != ABI_VERSION:
+        raise NativeError(f"libvss_amd ABI {L.vss_abi_version()} != expected {ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().vss_error_string(rc).decode()
+        raise NativeError(f"{what} failed: {msg} (code {rc})")
+
+
+def ptr(t: torch.Tensor | None):
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(device) -> torch.device:
+    """The product path runs on a ROCm GPU only (no CPU fallback)."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        raise NativeError(f"VSS runs on a ROCm GPU (got device {device}); there is no CPU path")
+    if not torch.cuda.is_available():
+        raise NativeError("VSS needs a ROCm GPU but torch.cuda.is_available() is False")
+    load()
+    return device

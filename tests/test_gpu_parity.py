@@ -1,0 +1,225 @@
+"""HIP step vs the CPU oracle, through the C ABI (needs a GPU: marked `gpu`).
+
+Bar: bit-exact for every output — integers (progress, reset, time-outs, dones, rng counter)
+and floats (state, observations, rewards) — because the kernel and the oracle evaluate the same
+float32 operation sequence with FMA contraction off.  Free-running rollouts therefore stay
+identical step after step (no teacher forcing needed).  At full size (65,536 fields) the tests
+check size-independent properties (invariants, determinism, draw statistics).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from vss_amd import _native as N
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def make_vss(n, max_len=400, seed=1234, weights=(10.0, 2.0, 3.0, 0.0)):
+    from envs.vss import VSS, default_cfg
+    cfg = default_cfg(n)
+    cfg["env"]["maxEpisodeLength"] = max_len
+    cfg["env"]["seed"] = seed
+    cfg["env"]["rew_weights"] = dict(goal=weights[0], grad=weights[1], move=weights[2], energy=weights[3])
+    return VSS(cfg, DEV, DEV, 0, True, False, False)
+
+
+def host_from(env) -> O.HostEnv:
+    h = O.HostEnv(env.num_fields)
+    h.state[:] = env.state.cpu().numpy()
+    h.progress[:] = env.progress_buf.cpu().numpy()
+    h.reset[:] = env.reset_buf.cpu().numpy()
+    h.dof[:] = env.dof_velocity_buf.reshape(-1, 12).cpu().numpy()
+    h.ctr[:] = env.rng_counter.cpu().numpy().view(np.uint32)
+    return h
+
+
+def oracle_params(env):
+    return O.params(env.w_goal, env.w_grad, env.w_move, env.w_energy, env.clip_actions,
+                    env.max_episode_length, env.seed)
+
+
+def assert_env_equal(env, h, msg=""):
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(env.state.cpu().numpy(), h.state, err_msg=msg + " state")
+    np.testing.assert_array_equal(env.progress_buf.cpu().numpy(), h.progress, err_msg=msg + " progress")
+    np.testing.assert_array_equal(env.reset_buf.cpu().numpy(), h.reset, err_msg=msg + " reset")
+    np.testing.assert_array_equal(env.dof_velocity_buf.reshape(-1, 12).cpu().numpy(), h.dof, err_msg=msg + " dof")
+    np.testing.assert_array_equal(env.rng_counter.cpu().numpy().view(np.uint32), h.ctr, err_msg=msg + " ctr")
+
+
+def bits(t):
+    return t.detach().cpu().numpy().view(np.uint32) if t.dtype == torch.float32 else t.detach().cpu().numpy()
+
+
+@pytest.mark.parametrize("n", [1, 63, 65, 4096])
+def test_construction_reset_and_observe_bit_exact(n):
+    env = make_vss(n)
+    h = O.HostEnv(n)
+    O.reset_dones(h, oracle_params(env))  # same template, external-reset purpose, ctr 0
+    assert_env_equal(env, h, "ctor")
+    for agents in (6, 3, 1):
+        want = O.compute_obs(h, agents)
+        got = env.compute_observations(torch.empty((n, agents, 52), device=DEV), agents)
+        np.testing.assert_array_equal(bits(got).reshape(want.shape), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("n,steps,max_len", [(4096, 200, 50), (65, 120, 30), (1, 60, 9)])
+def test_full_step_free_running_bit_exact(n, steps, max_len):
+    """Config 2 of BASELINE.json at 4,096 fields: random actions, free-running, every step."""
+    env = make_vss(n, max_len=max_len)
+    h = host_from(env)
+    prm = oracle_params(env)
+    gen = np.random.default_rng(n)
+    resets = goals = timeouts = 0
+    for t in range(steps):
+        a = gen.uniform(-1.3, 1.3, (n, 2, 3, 2)).astype(np.float32)
+        if t % 17 == 5:  # push some balls into the goals (play.py-style external writes)
+            k = max(1, n // 8)
+            env.ball_pos[:k] = torch.tensor([0.74, 0.05], device=DEV)
+            env.ball_vel[:k] = torch.tensor([1.0, 0.0], device=DEV)
+            h.state[0, :k], h.state[1, :k], h.state[2, :k], h.state[3, :k] = 0.74, 0.05, 1.0, 0.0
+        obs_dict, rew, reset, extras = env.step(torch.from_numpy(a).to(DEV))
+        io = O.make_io(n, O.MODE_FULL)
+        O.step(h, O.MODE_FULL, a.reshape(n, 12), io, prm)
+        msg = f"step {t}"
+        assert_env_equal(env, h, msg)
+        np.testing.assert_array_equal(bits(obs_dict["obs"]).reshape(n, 312), io["obs"].view(np.uint32).reshape(n, 312), err_msg=msg)
+        np.testing.assert_array_equal(bits(extras["terminal_observation"]).reshape(n, 312),
+                                      io["terminal_obs"].view(np.uint32).reshape(n, 312), err_msg=msg)
+        np.testing.assert_array_equal(bits(rew).reshape(n, 24), io["rew"].view(np.uint32), err_msg=msg)
+        np.testing.assert_array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), io["time_outs"], err_msg=msg)
+        np.testing.assert_array_equal(bits(extras["progress_buffer"]), io["progress_f"].view(np.uint32), err_msg=msg)
+        resets += int(h.reset.sum())
+        goals += int((np.abs(io["rew"][:, 0]) > 0).sum())
+        timeouts += int(io["time_outs"].sum())
+    assert resets > 0 and goals > 0 and timeouts > 0
+
+
+@pytest.mark.parametrize("mode", [O.MODE_SA, O.MODE_CMA, O.MODE_DMA])
+@pytest.mark.parametrize("n", [4096, 67])
+def test_wrapped_step_free_running_bit_exact(mode, n):
+    from envs.wrappers import SingleAgent, CMA, DMA
+    env = make_vss(n, max_len=40)
+    W = {O.MODE_SA: SingleAgent, O.MODE_CMA: CMA, O.MODE_DMA: DMA}[mode](env)
+    h = host_from(env)
+    prm = oracle_params(env)
+    gen = np.random.default_rng(100 + mode)
+    rows = 3 * n if mode == O.MODE_DMA else n
+    width = 6 if mode == O.MODE_CMA else 2
+    io = O.make_io(n, mode)
+    obs0 = W.reset()["obs"]
+    np.testing.assert_array_equal(bits(obs0).reshape(-1), O.compute_obs(h, 3 if mode == O.MODE_DMA else 1).view(np.uint32).reshape(-1))
+    for t in range(90):
+        a = gen.uniform(-1.2, 1.2, (rows, width)).astype(np.float32)
+        obs, reward, dones, info = W.step(torch.from_numpy(a).to(DEV))
+        O.step(h, mode, a, io, prm)
+        msg = f"mode {mode} step {t}"
+        assert_env_equal(env, h, msg)
+        np.testing.assert_array_equal(bits(W.action_buf).reshape(n, 12), io["ou_buf"].view(np.uint32), err_msg=msg)
+        np.testing.assert_array_equal(bits(obs["obs"]).reshape(-1), io["obs"].view(np.uint32).reshape(-1), err_msg=msg)
+        np.testing.assert_array_equal(bits(info["terminal_observation"]).reshape(-1), io["terminal_obs"].view(np.uint32).reshape(-1), err_msg=msg)
+        np.testing.assert_array_equal(bits(info["rews"]).reshape(-1), io["rew"].view(np.uint32).reshape(-1), err_msg=msg)
+        np.testing.assert_array_equal(bits(reward), io["reward_sum"].view(np.uint32), err_msg=msg)
+        np.testing.assert_array_equal(info["time_outs"].cpu().numpy().astype(np.uint8), io["time_outs"], err_msg=msg)
+        np.testing.assert_array_equal(bits(info["progress_buffer"]), io["progress_f"].view(np.uint32), err_msg=msg)
+        want_dones = io["dones_rep"] if mode == O.MODE_DMA else h.reset
+        np.testing.assert_array_equal(dones.cpu().numpy(), want_dones, err_msg=msg)
+        assert tuple(obs["obs"].shape) == (rows, 52) and tuple(dones.shape) == (rows,)
+    assert h.reset.sum() >= 0
+
+
+def test_external_reset_play_style():
+    """play.py:132-133: envs.reset_buf[:] = 1; envs.reset_dones() re-samples every field."""
+    n = 512
+    env = make_vss(n)
+    for _ in range(5):
+        env.step(torch.zeros((n, 2, 3, 2), device=DEV))
+    h = host_from(env)
+    env.reset_buf[:] = 1
+    h.reset[:] = 1
+    env.reset_dones()
+    O.reset_dones(h, oracle_params(env))
+    assert_env_equal(env, h, "external reset")
+
+
+def test_views_alias_state():
+    """ball_pos / robots_pos / ... are writable views of the state the kernel reads."""
+    env = make_vss(8)
+    env.robots_pos[3, 1, 2] = torch.tensor([0.25, -0.125], device=DEV)
+    env.ball_vel[2] = torch.tensor([0.5, 0.25], device=DEV)
+    env.robots_quats[1, 0, 1] = torch.tensor([0.0, 0.0, 0.6, 0.8], device=DEV)
+    s = env.state.cpu().numpy()
+    assert s[N.CH_RX + 5, 3] == 0.25 and s[N.CH_RY + 5, 3] == -0.125
+    assert s[N.CH_BALL_VX, 2] == 0.5 and s[N.CH_BALL_VY, 2] == 0.25
+    assert s[N.CH_RQZ + 1, 1] == np.float32(0.6) and s[N.CH_RQW + 1, 1] == np.float32(0.8)
+    assert tuple(env.robots_ang_vel.shape) == (8, 2, 3, 1)
+
+
+def test_full_size_invariants_and_determinism():
+    """65,536 fields (BASELINE config 3/4 size): bodies stay inside the walls, quaternions stay
+    unit, no NaN, goals / time-outs bookkeeping is consistent, and the same seed gives the
+    same bits."""
+    n = 65536
+    e1, e2 = make_vss(n, seed=77), make_vss(n, seed=77)
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    for t in range(120):
+        a = torch.rand((n, 2, 3, 2), device=DEV, generator=gen) * 2 - 1
+        o1, r1, d1, x1 = e1.step(a)
+        o2, r2, d2, x2 = e2.step(a)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.state, e2.state) and torch.equal(o1["obs"], o2["obs"])
+    s = e1.state
+    assert torch.isfinite(s).all() and torch.isfinite(o1["obs"]).all()
+    bx, by = s[0].abs(), s[1].abs()
+    assert (by <= 0.65 + 1e-4).all() and (bx <= 0.85 + 1e-4).all()
+    rx, ry = s[N.CH_RX:N.CH_RX + 6].abs(), s[N.CH_RY:N.CH_RY + 6].abs()
+    assert (ry <= 0.65 - 0.04 + 1e-4).all() and (rx <= 0.85 - 0.04 + 1e-4).all()
+    qn = s[N.CH_RQZ:N.CH_RQZ + 6] ** 2 + s[N.CH_RQW:N.CH_RQW + 6] ** 2
+    assert ((qn - 1).abs() < 1e-5).all()
+    assert (e1.progress_buf <= e1.max_episode_length).all()
+    # resets happen exactly where a goal or the episode limit fired
+    assert (x1["time_outs"] <= (d1 != 0)).all()
+
+
+def test_reset_distribution_matches_reference_statistics():
+    """Reset sampling (envs/vss.py:281-327): positions uniform in the +-field_scale/2 box with all
+    21 pair distances >= 0.07, yaw uniform, ball velocity U[-0.5, 0.5)^2 — checked by moments
+    over 65,536 fresh fields."""
+    n = 65536
+    env = make_vss(n, seed=99)
+    s = env.state.cpu().numpy().astype(np.float64)
+    xs = np.concatenate([s[0:1], s[N.CH_RX:N.CH_RX + 6]])
+    ys = np.concatenate([s[1:2], s[N.CH_RY:N.CH_RY + 6]])
+    assert np.abs(xs).max() <= 0.68 and np.abs(ys).max() <= 0.58
+    d = np.sqrt((xs[:, None] - xs[None]) ** 2 + (ys[:, None] - ys[None]) ** 2)
+    iu = np.triu_indices(7, 1)
+    assert d[iu].min() >= 0.07
+    # rejection conditions the marginals only slightly: mean ~0, var close to uniform's
+    assert abs(xs.mean()) < 0.01 and abs(ys.mean()) < 0.01
+    assert abs(xs.var() - 1.36 ** 2 / 12) < 0.01
+    yaw = 2 * np.arctan2(s[N.CH_RQZ:N.CH_RQZ + 6], s[N.CH_RQW:N.CH_RQW + 6])
+    yaw = (yaw + np.pi) % (2 * np.pi) - np.pi
+    assert abs(yaw.mean()) < 0.02 and abs(yaw.var() - np.pi ** 2 / 3) < 0.05
+    bv = s[2:4]
+    assert np.abs(bv).max() <= 0.5 and abs(bv.var() - 1 / 12) < 0.002
+    assert (s[N.CH_RVX:N.CH_RVX + 12] == 0).all() and (s[N.CH_RW:N.CH_RW + 6] == 0).all()
+
+
+def test_ou_noise_statistics():
+    """OU opponents (envs/wrappers.py:5-19): one step from zero gives clamp(N(0, 0.15^2))."""
+    from envs.wrappers import SingleAgent
+    n = 65536
+    env = make_vss(n, seed=5)
+    W = SingleAgent(env)
+    W.step(torch.zeros((n, 2), device=DEV))
+    ab = W.action_buf.reshape(n, 12).cpu().numpy().astype(np.float64)
+    done = env.reset_buf.cpu().numpy().astype(bool)
+    z = ab[~done][:, 2:]
+    assert np.all(ab[:, :2][~done] == 0)
+    assert abs(z.mean()) < 2e-3 and abs(z.std() - 0.15) < 2e-3
+    # 4th moment of a normal: 3 sigma^4
+    assert abs((z ** 4).mean() / 0.15 ** 4 - 3.0) < 0.1

@@ -1,0 +1,41 @@
+#!/usr/bin/env bash
+# One GPU-box session: GPU tests, smoke, bench, rocprofv3 kernel-trace stats.
+# Every GPU step has its own time limit; the script stops at the first abnormal exit
+# (fault / abort / segfault / timeout), and only continues past ordinary test failures.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p "$OUT"
+TAG=${TAG:-r01}
+
+run() {  # run <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*" | tee -a "$OUT/session.log"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a "$OUT/session.log"
+  tail -n 5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "abnormal exit ($rc) in $name: stopping" | tee -a "$OUT/session.log"
+    exit $rc
+  fi
+  return 0
+}
+
+STEPS=${STEPS:-tests,smoke,bench,prof}
+case ",$STEPS," in *,tests,*) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;; esac
+case ",$STEPS," in *,smoke,*) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;; esac
+case ",$STEPS," in *,bench,*) run bench 400 python bench.py ;; esac
+case ",$STEPS," in *,benchsa,*) run bench_sa 300 python bench.py --mode sa --no-cpu-baseline ;; esac
+case ",$STEPS," in *,prof,*)
+  run rocprof_stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \
+      python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline ;;
+esac
+case ",$STEPS," in *,pmc,*)
+  run rocprof_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$TAG" -o run -- \
+      python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline
+  run rocprof_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$TAG" -o run -- \
+      python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+esac
+echo "session done" | tee -a "$OUT/session.log"

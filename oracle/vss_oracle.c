@@ -195,7 +195,7 @@ static void contact_robot_robot(body_state* b, int i, int j) {
   if (!(d2 < O_RR_DIST2)) return;
   float d = sqrtf(d2);
   float nx = 1.0f, ny = 0.0f;
-  if (d > 1e-9f) { nx = dx / d; ny = dy / d; }
+  if (d > 1e-9f) { float inv = 1.0f / d; nx = dx * inv; ny = dy * inv; }
   float half = (O_RR_DIST - d) * 0.5f;
   b->x[i] = b->x[i] - nx * half; b->y[i] = b->y[i] - ny * half;
   b->x[j] = b->x[j] + nx * half; b->y[j] = b->y[j] + ny * half;
@@ -220,7 +220,8 @@ static void contact_ball_robot(body_state* b, int i) {
   if (d2 > 0.0f) {
     if (!(d2 < O_BALL_R2)) return;
     float d = sqrtf(d2);
-    nlx = ex / d; nly = ey / d;
+    float inv = 1.0f / d;
+    nlx = ex * inv; nly = ey * inv;
     pen = O_BALL_R - d;
   } else {
     float px = O_ROBOT_HALF - fabsf(lx), py = O_ROBOT_HALF - fabsf(ly);
@@ -252,7 +253,7 @@ static void contact_walls(float* x, float* y, float* vx, float* vy, float r) {
       if (d2 < r * r) {
         float d = sqrtf(d2);
         float nx = -1.0f, ny = 0.0f;
-        if (d > 1e-9f) { nx = dx / d; ny = dy / d; }
+        if (d > 1e-9f) { float inv = 1.0f / d; nx = dx * inv; ny = dy * inv; }
         float pen = r - d;
         ax = ax + nx * pen; ay = ay + ny * pen;
         float vn = avx * nx + avy * ny;
@@ -309,9 +310,9 @@ static void physics_field(body_state* b, const float a[12]) {
       oracle_sincosf(b->w[i] * O_HH, &sh, &ch);
       float qz = b->qz[i] * ch + b->qw[i] * sh;
       float qw = b->qw[i] * ch - b->qz[i] * sh;
-      float nrm = sqrtf(qz * qz + qw * qw);
-      b->qz[i] = qz / nrm;
-      b->qw[i] = qw / nrm;
+      float k = 1.5f - 0.5f * (qz * qz + qw * qw); /* one Newton step of 1/|q| */
+      b->qz[i] = qz * k;
+      b->qw[i] = qw * k;
       heading(b, i);
     }
     b->bx = b->bx + b->bvx * O_H;

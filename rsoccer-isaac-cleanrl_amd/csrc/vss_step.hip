@@ -173,7 +173,7 @@ __device__ __forceinline__ void contact_robot_robot(Bodies& b, int i, int j) {
   if (d2 < K_RR_DIST2) {
     float d = sqrtf(d2);
     float nx = 1.0f, ny = 0.0f;
-    if (d > 1e-9f) { nx = dx / d; ny = dy / d; }
+    if (d > 1e-9f) { float inv = 1.0f / d; nx = dx * inv; ny = dy * inv; }
     float half = (K_RR_DIST - d) * 0.5f;
     b.x[i] = b.x[i] - nx * half; b.y[i] = b.y[i] - ny * half;
     b.x[j] = b.x[j] + nx * half; b.y[j] = b.y[j] + ny * half;
@@ -195,20 +195,18 @@ __device__ __forceinline__ void contact_ball_robot(Bodies& b, int i) {
   float cy = clampf(ly, -K_ROBOT_HALF, K_ROBOT_HALF);
   float ex = lx - cx, ey = ly - cy;
   float d2 = ex * ex + ey * ey;
-  float nlx, nly, pen;
-  bool hit;
-  if (d2 > 0.0f) {
-    hit = d2 < K_BALL_R2;
-    float d = sqrtf(d2);
-    nlx = ex / d; nly = ey / d;
-    pen = K_BALL_R - d;
-  } else {
-    hit = true;
-    float px = K_ROBOT_HALF - fabsf(lx), py = K_ROBOT_HALF - fabsf(ly);
-    if (px < py) { nlx = lx >= 0.0f ? 1.0f : -1.0f; nly = 0.0f; pen = px + K_BALL_R; }
-    else { nlx = 0.0f; nly = ly >= 0.0f ? 1.0f : -1.0f; pen = py + K_BALL_R; }
-  }
-  if (hit) {
+  if (d2 < K_BALL_R2) {  // contact (d2 == 0: ball centre inside the box)
+    float nlx, nly, pen;
+    if (d2 > 0.0f) {
+      float d = sqrtf(d2);
+      float inv = 1.0f / d;
+      nlx = ex * inv; nly = ey * inv;
+      pen = K_BALL_R - d;
+    } else {
+      float px = K_ROBOT_HALF - fabsf(lx), py = K_ROBOT_HALF - fabsf(ly);
+      if (px < py) { nlx = lx >= 0.0f ? 1.0f : -1.0f; nly = 0.0f; pen = px + K_BALL_R; }
+      else { nlx = 0.0f; nly = ly >= 0.0f ? 1.0f : -1.0f; pen = py + K_BALL_R; }
+    }
     float nx = c * nlx - s * nly;
     float ny = s * nlx + c * nly;
     float pr = pen * K_W_ROBOT_BR, pb = pen * K_W_BALL_BR;
@@ -235,7 +233,7 @@ __device__ __forceinline__ void contact_walls(float& x, float& y, float& vx, flo
       if (d2 < r * r) {
         float d = sqrtf(d2);
         float nx = -1.0f, ny = 0.0f;
-        if (d > 1e-9f) { nx = dx / d; ny = dy / d; }
+        if (d > 1e-9f) { float inv = 1.0f / d; nx = dx * inv; ny = dy * inv; }
         float pen = r - d;
         ax = ax + nx * pen; ay = ay + ny * pen;
         float vn = avx * nx + avy * ny;
@@ -295,9 +293,9 @@ __device__ __forceinline__ void physics(Bodies& b, const float a[12]) {
       sincos_small(b.w[i] * K_HH, sh, ch);
       float qz = b.qz[i] * ch + b.qw[i] * sh;
       float qw = b.qw[i] * ch - b.qz[i] * sh;
-      float nrm = sqrtf(qz * qz + qw * qw);
-      b.qz[i] = qz / nrm;
-      b.qw[i] = qw / nrm;
+      float k = 1.5f - 0.5f * (qz * qz + qw * qw);  // one Newton step of 1/|q|
+      b.qz[i] = qz * k;
+      b.qw[i] = qw * k;
       heading(b, i);
     }
     b.bx = b.bx + b.bvx * K_H;
@@ -549,7 +547,9 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   for (int i = 0; i < 6; ++i) { prx[i] = b.x[i]; pry[i] = b.y[i]; }
 
   // -- gym.simulate replacement ------------------------------------------------------------------------
+#ifndef VSS_PROF_SKIP_PHYSICS  // profiling-only ablation knobs (tools/ablate.py); never set in the product
   if (valid) physics(b, a);
+#endif
 
   // -- post_physics_step: progress, rewards, dones (envs/vss.py:189-265) ----------------------------------
   progress += 1;
@@ -586,7 +586,9 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   // -- terminal observation (envs/vss.py:195-196) ----------------------------------------------------------
   write_obs_record(rec, b, a);
   __syncthreads();
+#ifndef VSS_PROF_SKIP_OBS
   coop_store_obs<A>(args.io.terminal_obs + f0 * (52 * A), nv, lds, lane);
+#endif
   __syncthreads();
 
   // -- reset_dones (envs/vss.py:202, 267-333) ---------------------------------------------------------------
@@ -602,7 +604,9 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   // -- observation after reset (envs/vss.py:203) -------------------------------------------------------------
   write_obs_record(rec, b, dof);
   __syncthreads();
+#ifndef VSS_PROF_SKIP_OBS
   coop_store_obs<A>(args.io.obs + f0 * (52 * A), nv, lds, lane);
+#endif
   __syncthreads();
 
   // -- bookkeeping --------------------------------------------------------------------------------------------

@@ -1,0 +1,362 @@
+"""Drop-in PPO train loop (cleanrl ppo_continuous_action_isaacgym, as used by the reference's
+ppo_continuous_action_isaacgym.py) on the MI355X VSS env.
+
+Same command line (`--env-id sa|cma|dma --num-envs ... --num-steps ...`, ppo…:48-118), same
+`Agent` (module order, orthogonal init, state-dict keys: ppo…:121-164), same rollout / GAE /
+clipped-PPO update semantics (ppo…:231-365).  MI355X-first changes:
+
+* the env is the fused HIP step (envs/wrappers.py), one launch per control step;
+* data parallel over ranks (one process per GPU, `torch.distributed` = RCCL): each rank owns
+  `--num-envs` environments (weak scaling; BASELINE config 5 = 8 x 65,536) and its own rollout
+  storage; the only exchange is ONE all-reduce of a flat fp32 gradient buffer per minibatch
+  (all parameter .grad tensors are views into it), between backward() and clip_grad_norm_
+  (ppo…:352-353); approx_kl is averaged over ranks when it drives a decision;
+* no per-element host-synchronising logging loop (ppo…:273-279): episode statistics are
+  reduced on the device and read once per update;
+* logging is optional (TensorBoard / W&B only if installed and requested).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import random
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.optim as optim
+from torch.distributions.normal import Normal
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from envs._gym import Box, ObservationWrapper  # noqa: E402
+
+
+def strtobool(x: str) -> bool:
+    v = str(x).lower()
+    if v in ("y", "yes", "t", "true", "on", "1"):
+        return True
+    if v in ("n", "no", "f", "false", "off", "0"):
+        return False
+    raise ValueError(f"invalid truth value {x!r}")
+
+
+def parse_args(argv=None):
+    b = strtobool
+    p = argparse.ArgumentParser()
+    p.add_argument("--exp-name", type=str, default=os.path.basename(__file__).rstrip(".py"))
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--torch-deterministic", type=b, default=True, nargs="?", const=True)
+    p.add_argument("--cuda", type=b, default=True, nargs="?", const=True)
+    p.add_argument("--track", type=b, default=False, nargs="?", const=True)
+    p.add_argument("--wandb-project-name", type=str, default="ppo-isaac-cleanrl")
+    p.add_argument("--wandb-entity", type=str, default=None)
+    p.add_argument("--capture-video", type=b, default=False, nargs="?", const=True)
+    p.add_argument("--env-id", type=str, default="sa")
+    p.add_argument("--total-timesteps", type=int, default=1000000000)
+    p.add_argument("--learning-rate", type=float, default=0.001)
+    p.add_argument("--num-envs", type=int, default=4095, help="environments per rank")
+    p.add_argument("--num-steps", type=int, default=128)
+    p.add_argument("--anneal-lr", type=b, default=False, nargs="?", const=True)
+    p.add_argument("--adaptative-lr", type=b, default=False, nargs="?", const=True)
+    p.add_argument("--gamma", type=float, default=0.99)
+    p.add_argument("--gae-lambda", type=float, default=0.95)
+    p.add_argument("--num-minibatches", type=int, default=4)
+    p.add_argument("--update-epochs", type=int, default=8)
+    p.add_argument("--norm-adv", type=b, default=True, nargs="?", const=True)
+    p.add_argument("--clip-coef", type=float, default=0.2)
+    p.add_argument("--clip-vloss", type=b, default=False, nargs="?", const=True)
+    p.add_argument("--ent-coef", type=float, default=0.005)
+    p.add_argument("--vf-coef", type=float, default=4)
+    p.add_argument("--max-grad-norm", type=float, default=1.5)
+    p.add_argument("--target-kl", type=float, default=None)
+    p.add_argument("--threshold-kl", type=float, default=0.008)
+    p.add_argument("--reward-scaler", type=float, default=1000)
+    p.add_argument("--record-video-step-frequency", type=int, default=20000)
+    p.add_argument("--test", type=b, default=False, nargs="?", const=True)
+    # build additions
+    p.add_argument("--save-path", type=str, default="runs")
+    p.add_argument("--num-updates", type=int, default=None, help="override total_timesteps // batch")
+    p.add_argument("--log", type=b, default=True, nargs="?", const=True)
+    args = p.parse_args(argv)
+    args.batch_size = int(args.num_envs * args.num_steps)
+    args.minibatch_size = int(args.batch_size // args.num_minibatches)
+    return args
+
+
+def layer_init(layer, std=np.sqrt(2), bias_const=0.0):
+    torch.nn.init.orthogonal_(layer.weight, std)
+    torch.nn.init.constant_(layer.bias, bias_const)
+    return layer
+
+
+def _mlp(n_in, n_out, last_std):
+    return nn.Sequential(
+        layer_init(nn.Linear(n_in, 256)), nn.Tanh(),
+        layer_init(nn.Linear(256, 512)), nn.Tanh(),
+        layer_init(nn.Linear(512, 512)), nn.Tanh(),
+        layer_init(nn.Linear(512, 256)), nn.Tanh(),
+        layer_init(nn.Linear(256, n_out), std=last_std),
+    )
+
+
+class Agent(nn.Module):
+    """Separate actor / critic MLPs with a state-independent log-std (ppo…:127-164)."""
+
+    def __init__(self, envs):
+        super().__init__()
+        n_obs = int(np.array(envs.single_observation_space.shape).prod())
+        n_act = int(np.prod(envs.single_action_space.shape))
+        self.critic = _mlp(n_obs, 1, 1.0)       # created first: same RNG consumption order
+        self.actor_mean = _mlp(n_obs, n_act, 0.01)
+        self.actor_logstd = nn.Parameter(torch.zeros(1, n_act))
+
+    def get_value(self, x):
+        return self.critic(x)
+
+    def get_action_and_value(self, x, action=None):
+        mean = self.actor_mean(x)
+        std = torch.exp(self.actor_logstd.expand_as(mean))
+        probs = Normal(mean, std)
+        if action is None:
+            action = probs.sample()
+        return action, probs.log_prob(action).sum(1), probs.entropy().sum(1), self.critic(x)
+
+
+class ExtractObsWrapper(ObservationWrapper):
+    def observation(self, obs):
+        return obs["obs"]
+
+
+class FlatGrads:
+    """All parameter gradients as views of ONE contiguous fp32 buffer, so the data-parallel
+    exchange is a single all-reduce (4.3 MB for the SA agent) with no pack/unpack copies."""
+
+    def __init__(self, module: nn.Module):
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        total = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(total, device=self.params[0].device, dtype=torch.float32)
+        off = 0
+        for p in self.params:
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+
+    def zero(self):
+        self.flat.zero_()
+
+    def all_reduce_mean(self, world: int):
+        if world > 1:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
+            self.flat.mul_(1.0 / world)
+
+
+class _NullWriter:
+    def add_scalar(self, *a, **k):
+        pass
+
+    def add_text(self, *a, **k):
+        pass
+
+    def close(self):
+        pass
+
+
+def make_writer(args, run_name, rank):
+    if rank != 0 or not args.log:
+        return _NullWriter()
+    try:
+        from torch.utils.tensorboard import SummaryWriter
+        return SummaryWriter(f"{args.save_path}/{run_name}")
+    except Exception:  # tensorboard not installed
+        return _NullWriter()
+
+
+def compute_gae(rewards, values, next_values, next_dones, next_timeouts, gamma, lam):
+    """Timeout-aware GAE of ppo…:282-296 (terminal-obs bootstrap, reversed scan over T)."""
+    T = rewards.shape[0]
+    advantages = torch.zeros_like(rewards)
+    next_non_terminal = 1.0 - next_dones.logical_and(next_timeouts.logical_not()).float()
+    lastgaelam = torch.zeros_like(rewards[0])
+    for t in reversed(range(T)):
+        delta = rewards[t] + gamma * next_values[t] * next_non_terminal[t] - values[t]
+        lastgaelam = delta + gamma * lam * (1.0 - next_dones[t]) * lastgaelam
+        advantages[t] = lastgaelam
+    return advantages, advantages + values
+
+
+def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_advantages, b_returns,
+               b_values, world=1, gen=None):
+    """Clipped PPO over update_epochs x num_minibatches (ppo…:306-365).  Returns last-minibatch
+    stats.  `flat` holds the grads; with world > 1 it is all-reduced before clipping."""
+    device = b_obs.device
+    batch = b_obs.shape[0]
+    mb = batch // args.num_minibatches
+    clipfracs = []
+    stats = {}
+    for epoch in range(args.update_epochs):
+        b_inds = torch.randperm(batch, device=device, generator=gen)
+        for start in range(0, batch, mb):
+            mb_inds = b_inds[start:start + mb]
+            _, newlogprob, entropy, newvalue = agent.get_action_and_value(b_obs[mb_inds], b_actions[mb_inds])
+            logratio = newlogprob - b_logprobs[mb_inds]
+            ratio = logratio.exp()
+            with torch.no_grad():
+                old_approx_kl = (-logratio).mean()
+                approx_kl = ((ratio - 1) - logratio).mean()
+                clipfracs.append(((ratio - 1.0).abs() > args.clip_coef).float().mean())
+            mb_adv = b_advantages[mb_inds]
+            if args.norm_adv:
+                mb_adv = (mb_adv - mb_adv.mean()) / (mb_adv.std() + 1e-8)
+            pg_loss = torch.max(-mb_adv * ratio, -mb_adv * torch.clamp(ratio, 1 - args.clip_coef, 1 + args.clip_coef)).mean()
+            newvalue = newvalue.view(-1)
+            if args.clip_vloss:
+                v_unclipped = (newvalue - b_returns[mb_inds]) ** 2
+                v_clipped = b_values[mb_inds] + torch.clamp(newvalue - b_values[mb_inds], -args.clip_coef, args.clip_coef)
+                v_loss = 0.5 * torch.max(v_unclipped, (v_clipped - b_returns[mb_inds]) ** 2).mean()
+            else:
+                v_loss = 0.5 * ((newvalue - b_returns[mb_inds]) ** 2).mean()
+            entropy_loss = entropy.mean()
+            loss = pg_loss - args.ent_coef * entropy_loss + v_loss * args.vf_coef
+
+            flat.zero()
+            loss.backward()
+            flat.all_reduce_mean(world)  # the data-parallel exchange (RCCL on ROCm)
+            nn.utils.clip_grad_norm_(agent.parameters(), args.max_grad_norm)
+            optimizer.step()
+
+            if args.adaptative_lr or args.target_kl is not None:
+                if world > 1:
+                    dist.all_reduce(approx_kl, op=dist.ReduceOp.SUM)
+                    approx_kl /= world
+            if args.adaptative_lr:
+                lr = optimizer.param_groups[0]["lr"]
+                kl = float(approx_kl)
+                if kl > 2.0 * args.threshold_kl:
+                    optimizer.param_groups[0]["lr"] = max(lr / 1.5, 1e-6)
+                elif kl < 0.5 * args.threshold_kl:
+                    optimizer.param_groups[0]["lr"] = min(lr * 1.5, 1e-2)
+        if args.target_kl is not None and float(approx_kl) > args.target_kl:
+            break
+    stats.update(v_loss=v_loss.detach(), pg_loss=pg_loss.detach(), entropy=entropy_loss.detach(),
+                 old_approx_kl=old_approx_kl, approx_kl=approx_kl,
+                 clipfrac=torch.stack(clipfracs).mean())
+    return stats
+
+
+def setup_distributed():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {"device_id": torch.device(f"cuda:{local}")} if backend == "nccl" else {}
+        dist.init_process_group(backend, **kw)
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    return world, rank, local
+
+
+def train(args):
+    world, rank, local = setup_distributed()
+    run_name = f"{args.exp_name}_ppo-{args.env_id}_{args.seed}"
+    writer = make_writer(args, run_name, rank)
+    writer.add_text("hyperparameters", "|param|value|\n|-|-|\n%s" % "\n".join(f"|{k}|{v}|" for k, v in vars(args).items()))
+
+    seed = args.seed + rank
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(args.seed)  # same initial weights on every rank
+    torch.backends.cudnn.deterministic = args.torch_deterministic
+    device = torch.device(f"cuda:{local}" if torch.cuda.is_available() and args.cuda else "cpu")
+
+    from envs.wrappers import RecordEpisodeStatisticsTorch, make_env
+    unwrapped_env, envs = make_env(args)
+    envs = ExtractObsWrapper(envs)
+    envs = RecordEpisodeStatisticsTorch(envs, device)
+    envs.single_action_space = envs.action_space
+    envs.single_observation_space = envs.observation_space
+    assert isinstance(envs.single_action_space, Box), "only continuous action space is supported"
+
+    agent = Agent(envs).to(device)
+    flat = FlatGrads(agent)
+    optimizer = optim.Adam(agent.parameters(), lr=args.learning_rate, eps=1e-5)
+    gen = torch.Generator(device=device).manual_seed(seed)
+
+    T, E = args.num_steps, args.num_envs
+    obs_dim = envs.single_observation_space.shape
+    act_dim = envs.single_action_space.shape
+    obs = torch.zeros((T, E) + obs_dim, device=device)
+    actions = torch.zeros((T, E) + act_dim, device=device)
+    logprobs = torch.zeros((T, E), device=device)
+    rewards = torch.zeros((T, E), device=device)
+    next_dones = torch.zeros((T, E), device=device)
+    next_timeouts = torch.zeros((T, E), device=device)
+    values = torch.zeros((T, E), device=device)
+    next_values = torch.zeros((T, E), device=device)
+
+    global_step = 0
+    start_time = time.time()
+    next_obs = envs.reset()
+    num_updates = args.num_updates if args.num_updates is not None else args.total_timesteps // (args.batch_size * world)
+    history = []
+    for update in range(1, num_updates + 1):
+        if args.anneal_lr:
+            optimizer.param_groups[0]["lr"] = (1.0 - (update - 1.0) / num_updates) * args.learning_rate
+        t_roll = time.time()
+        ep_ret = torch.zeros((), device=device)
+        ep_cnt = torch.zeros((), device=device)
+        for step in range(T):
+            global_step += E * world
+            obs[step] = next_obs
+            with torch.no_grad():
+                action, logprob, _, value = agent.get_action_and_value(next_obs)
+                values[step] = value.flatten()
+            actions[step] = action
+            logprobs[step] = logprob
+            next_obs, rewards[step], next_done, info = envs.step(action)
+            next_dones[step] = next_done
+            next_timeouts[step] = info["time_outs"]
+            with torch.no_grad():
+                next_values[step] = agent.get_value(info["terminal_observation"]).reshape(1, -1)
+            d = next_done.float()
+            ep_ret += (info["r"]["return"] * d).sum()
+            ep_cnt += d.sum()
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+        t_roll = time.time() - t_roll
+
+        with torch.no_grad():
+            advantages, returns = compute_gae(rewards, values, next_values, next_dones, next_timeouts,
+                                              args.gamma, args.gae_lambda)
+        t_upd = time.time()
+        stats = ppo_update(agent, optimizer, flat, args, obs.reshape((-1,) + obs_dim), logprobs.reshape(-1),
+                           actions.reshape((-1,) + act_dim), advantages.reshape(-1), returns.reshape(-1),
+                           values.reshape(-1), world=world, gen=gen)
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+        t_upd = time.time() - t_upd
+        sps = int(global_step / (time.time() - start_time))
+        rec = {"update": update, "global_step": global_step, "sps": sps, "rollout_s": t_roll, "update_s": t_upd,
+               "episodes": float(ep_cnt), "mean_return": float(ep_ret / ep_cnt.clamp(min=1)),
+               **{k: float(v) for k, v in stats.items()}}
+        history.append(rec)
+        for k in ("v_loss", "pg_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac"):
+            writer.add_scalar(f"losses/{k if k != 'v_loss' else 'value_loss'}", rec[k], global_step)
+        writer.add_scalar("losses/learning_rate", optimizer.param_groups[0]["lr"], global_step)
+        writer.add_scalar("Charts/SPS", sps, global_step)
+        if rank == 0 and args.log:
+            print(f"update {update}/{num_updates} step {global_step} SPS {sps} rollout {t_roll:.2f}s "
+                  f"update {t_upd:.2f}s return {rec['mean_return']:.3f} kl {rec['approx_kl']:.4f}", flush=True)
+
+    if rank == 0 and args.log:
+        os.makedirs(f"{args.save_path}/{run_name}", exist_ok=True)
+        torch.save(agent.state_dict(), f"{args.save_path}/{run_name}/{run_name}-agent.pt")
+    writer.close()
+    return agent, history
+
+
+if __name__ == "__main__":
+    train(parse_args())

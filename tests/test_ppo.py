@@ -1,0 +1,176 @@
+"""PPO drop-in (ppo_continuous_action_isaacgym.py): Agent parity with the reference (golden G6),
+GAE known answers, the flat-gradient data-parallel update (gloo, world size 2, CPU), and a short
+end-to-end training run on the GPU."""
+import os
+import socket
+from collections import namedtuple
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import ppo_continuous_action_isaacgym as P
+from envs._gym import Box
+
+Env = namedtuple("Env", ["single_observation_space", "single_action_space"])
+
+
+def make_agent(act_dim, seed=42):
+    torch.manual_seed(seed)
+    return P.Agent(Env(Box(-np.inf, np.inf, (52,)), Box(-1.0, 1.0, (act_dim,))))
+
+
+@pytest.mark.parametrize("act_dim", [2, 6])
+def test_agent_matches_reference_init_and_forward(golden_dir, act_dim):
+    """Same modules, creation order, orthogonal init and state-dict keys as the reference Agent
+    (ppo…:121-164): from torch.manual_seed(42) the parameters and the forward outputs match."""
+    g = np.load(os.path.join(golden_dir, "g6_agent.npz"), allow_pickle=False)
+    agent = make_agent(act_dim)
+    sd = agent.state_dict()
+    assert list(sd.keys()) == list(g[f"a{act_dim}_keys"])
+    assert [str(tuple(v.shape)) for v in sd.values()] == list(g[f"a{act_dim}_shapes"])
+    assert sum(v.numel() for v in sd.values()) == int(g[f"a{act_dim}_nparams"])
+    np.testing.assert_allclose([float(v.double().sum()) for v in sd.values()], g[f"a{act_dim}_param_sums"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose([float(v.double().abs().sum()) for v in sd.values()], g[f"a{act_dim}_param_abs_sums"], rtol=1e-6)
+    x = torch.from_numpy(g[f"a{act_dim}_x"])
+    a = torch.from_numpy(g[f"a{act_dim}_a"])
+    with torch.no_grad():
+        _, logp, ent, val = agent.get_action_and_value(x, a)
+        mean = agent.actor_mean(x)
+    np.testing.assert_allclose(mean.numpy(), g[f"a{act_dim}_mean"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(logp.numpy(), g[f"a{act_dim}_logp"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ent.numpy(), g[f"a{act_dim}_ent"], rtol=1e-6)
+    np.testing.assert_allclose(val.numpy(), g[f"a{act_dim}_val"], rtol=1e-5, atol=1e-6)
+
+
+def test_gae_known_answers():
+    """Timeout-aware GAE (ppo…:282-296), hand-computed on T=3, two envs."""
+    gamma, lam = 0.9, 0.5
+    rewards = torch.tensor([[1.0, 0.0], [0.0, 2.0], [1.0, 1.0]])
+    values = torch.tensor([[0.5, 0.1], [0.2, 0.3], [0.4, 0.0]])
+    next_values = torch.tensor([[0.2, 0.3], [0.7, 0.9], [1.0, 2.0]])
+    next_dones = torch.tensor([[0.0, 0.0], [1.0, 0.0], [0.0, 1.0]])
+    next_timeouts = torch.tensor([[0.0, 0.0], [1.0, 0.0], [0.0, 0.0]])
+    adv, ret = P.compute_gae(rewards, values, next_values, next_dones, next_timeouts, gamma, lam)
+    # env 0: t=2: d=1+0.9*1*1-0.4=1.5; t=1 (done by timeout -> bootstrap kept, chain cut):
+    # d=0+0.9*0.7-0.2=0.43, A1=0.43; t=0: d=1+0.9*0.2-0.5=0.68, A0=0.68+0.45*0.43=0.8735
+    # env 1: t=2 terminal (no bootstrap): d=1+0-0=1; t=1: d=2+0.9*0.9-0.3=2.51, A1=2.51+0.45*1=2.96
+    # t=0: d=0+0.9*0.3-0.1=0.17, A0=0.17+0.45*2.96=1.502
+    want = torch.tensor([[0.8735, 1.502], [0.43, 2.96], [1.5, 1.0]])
+    torch.testing.assert_close(adv, want, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(ret, want + values)
+
+
+def test_flat_grads_are_views():
+    agent = make_agent(2)
+    flat = P.FlatGrads(agent)
+    assert flat.flat.numel() == 1079045
+    loss = agent.get_action_and_value(torch.randn(8, 52))[3].sum()
+    flat.zero()
+    loss.backward()
+    assert flat.flat.abs().sum() > 0
+    off = 0
+    for p in agent.parameters():
+        assert p.grad.data_ptr() == flat.flat[off:off + p.numel()].data_ptr()
+        off += p.numel()
+
+
+def _args(**kw):
+    a = P.parse_args([])
+    a.update_epochs, a.num_minibatches = 2, 2
+    for k, v in kw.items():
+        setattr(a, k, v)
+    return a
+
+
+def _synthetic_batch(seed, n=256):
+    g = torch.Generator().manual_seed(seed)
+    obs = torch.randn(n, 52, generator=g)
+    act = torch.randn(n, 2, generator=g) * 0.5
+    return obs, act, torch.randn(n, generator=g) - 3.0, torch.randn(n, generator=g), \
+        torch.randn(n, generator=g), torch.randn(n, generator=g)
+
+
+def _dp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    agent = make_agent(2)
+    flat = P.FlatGrads(agent)
+    opt = torch.optim.Adam(agent.parameters(), lr=1e-3, eps=1e-5)
+    args = _args(norm_adv=False)
+    obs, act, logp, adv, ret, val = _synthetic_batch(100 + rank)
+    P.ppo_update(agent, opt, flat, args, obs, logp, act, adv, ret, val, world=world,
+                 gen=torch.Generator().manual_seed(7))
+    q.put((rank, torch.cat([p.detach().reshape(-1) for p in agent.parameters()]).numpy()))
+    torch.distributed.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_data_parallel_update_gloo_world2():
+    """Two ranks with different local batches end with identical weights (one all-reduce per
+    minibatch keeps replicas in sync), and those weights equal a single process that averages
+    the two ranks' gradients by hand."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    np.testing.assert_array_equal(out[0], out[1])
+
+    # reference: the same two minibatch streams, gradients averaged explicitly
+    torch.manual_seed(0)
+    agents = [make_agent(2), make_agent(2)]
+    agents[1].load_state_dict(agents[0].state_dict())
+    flats = [P.FlatGrads(a) for a in agents]
+    opt = torch.optim.Adam(agents[0].parameters(), lr=1e-3, eps=1e-5)
+    args = _args(norm_adv=False)
+    data = [_synthetic_batch(100 + r) for r in range(2)]
+    gens = [torch.Generator().manual_seed(7) for _ in range(2)]
+    for epoch in range(args.update_epochs):
+        perms = [torch.randperm(256, generator=gg) for gg in gens]
+        for start in range(0, 256, 128):
+            for r in range(2):
+                obs, act, logp, adv, ret, val = data[r]
+                mb = perms[r][start:start + 128]
+                _, nl, ent, nv = agents[r].get_action_and_value(obs[mb], act[mb])
+                ratio = (nl - logp[mb]).exp()
+                pg = torch.max(-adv[mb] * ratio, -adv[mb] * torch.clamp(ratio, 0.8, 1.2)).mean()
+                vl = 0.5 * ((nv.view(-1) - ret[mb]) ** 2).mean()
+                loss = pg - args.ent_coef * ent.mean() + vl * args.vf_coef
+                flats[r].zero()
+                loss.backward()
+            avg = (flats[0].flat + flats[1].flat) / 2
+            flats[0].flat.copy_(avg)
+            torch.nn.utils.clip_grad_norm_(agents[0].parameters(), args.max_grad_norm)
+            opt.step()
+            agents[1].load_state_dict(agents[0].state_dict())
+    want = torch.cat([p.detach().reshape(-1) for p in agents[0].parameters()]).numpy()
+    np.testing.assert_allclose(out[0], want, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env_id", ["sa", "cma", "dma"])
+def test_train_end_to_end_gpu(env_id, tmp_path):
+    """Two PPO updates on the HIP env (small config): finite losses, rewards flow, SPS > 0."""
+    args = P.parse_args(["--env-id", env_id, "--num-envs", "3072", "--num-steps", "16",
+                         "--update-epochs", "2", "--num-updates", "2", "--save-path", str(tmp_path)])
+    agent, hist = P.train(args)
+    assert len(hist) == 2
+    for h in hist:
+        for k in ("v_loss", "pg_loss", "entropy", "approx_kl"):
+            assert np.isfinite(h[k]), (k, h)
+        assert h["sps"] > 0
+    assert os.path.exists(os.path.join(tmp_path, f"{args.exp_name}_ppo-{env_id}_1", f"{args.exp_name}_ppo-{env_id}_1-agent.pt"))

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Profiling-only: time ablated builds of the step kernel (VSS_PROF_* knobs) at 65,536 fields.
+
+Builds each variant of csrc/vss_step.hip into tools/_build/, loads it with ctypes beside the
+product library and times `vss_step` (FULL) with HIP events.  The numbers say which phase the
+kernel's time goes to; the ablated outputs are wrong by construction and never used."""
+import ctypes
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "rsoccer-isaac-cleanrl_amd"))
+import torch  # noqa: E402
+
+from vss_amd import _native as N  # noqa: E402
+
+VARIANTS = {"full": [], "no_physics": ["-DVSS_PROF_SKIP_PHYSICS"], "no_obs": ["-DVSS_PROF_SKIP_OBS"],
+            "no_physics_no_obs": ["-DVSS_PROF_SKIP_PHYSICS", "-DVSS_PROF_SKIP_OBS"]}
+EXTRA = [v for v in os.environ.get("ABLATE_EXTRA", "").split(",") if v]
+
+
+def build(name, flags):
+    out = os.path.join(REPO, "tools", "_build", f"libvss_{name}.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    src = os.path.join(REPO, "rsoccer-isaac-cleanrl_amd", "csrc", "vss_step.hip")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-shared",
+                    "-ffp-contract=off", *flags, "-o", out, src], check=True)
+    return out
+
+
+def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "build":
+        for k, v in VARIANTS.items():
+            build(k, v)
+        return
+    from envs.vss import VSS, default_cfg
+    n = int(os.environ.get("FIELDS", 65536))
+    cfg = default_cfg(n)
+    cfg["env"]["seed"] = 3
+    env = VSS(cfg, "cuda:0", "cuda:0", 0, True, False, False)
+    acts = torch.rand((n, 12), device="cuda:0") * 2 - 1
+    prm, st = env._c_params(), env._c_state()
+    io = N.VssStepIO(acts.data_ptr(), None, env.obs_buf.data_ptr(), env.terminal_obs_buf.data_ptr(),
+                     env.rew_buf.data_ptr(), None, None, env.timeout_buf.data_ptr(), env.progress_f_buf.data_ptr())
+    stream = N.stream_of(env.device)
+    for name in VARIANTS:
+        path = os.path.join(REPO, "tools", "_build", f"libvss_{name}.so")
+        L = ctypes.CDLL(path)
+        L.vss_step.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32] + [ctypes.c_void_p] * 3
+        for _ in range(20):
+            L.vss_step(stream, n, 0, ctypes.byref(prm), ctypes.byref(st), ctypes.byref(io))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        K = 100
+        for _ in range(K):
+            L.vss_step(stream, n, 0, ctypes.byref(prm), ctypes.byref(st), ctypes.byref(io))
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"{name:20s} {e0.elapsed_time(e1) / K * 1e3:8.1f} us/step")
+
+
+if __name__ == "__main__":
+    main()

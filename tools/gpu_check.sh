@@ -38,4 +38,6 @@ case ",$STEPS," in *,pmc,*)
   run rocprof_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$TAG" -o run -- \
       python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
 esac
+ case ",$STEPS," in *,ablate,*) run ablate 300 python tools/ablate.py ;; esac
+case ",$STEPS," in *,ppo,*) run ppo_sa 900 python rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 2 --save-path /tmp/runs ;; esac
 echo "session done" | tee -a "$OUT/session.log"

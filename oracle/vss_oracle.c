@@ -17,9 +17,9 @@
  * Constants.  Reference values: envs/vss.py:48-49 (42 rad/s, 0.07 m), 342-345 (field),
  * envs/vss.yaml:6-16, envs/vss_robot.urdf (robot).  Model constants: DESIGN.md §3.
  * ---------------------------------------------------------------------------------------- */
-#define O_NSUB 4
-#define O_H 0.0125f           /* dt / NSUB, dt = 0.05 (envs/vss.yaml:16) */
-#define O_HH 0.00625f         /* H / 2 (half-angle step)                 */
+#define O_NSUB 2
+#define O_H 0.025f            /* dt / NSUB, dt = 0.05 (envs/vss.yaml:16); 2 substeps as Isaac Gym */
+#define O_HH 0.0125f          /* H / 2 (half-angle step)                 */
 #define O_FIELD_HX 0.75f      /* field_width / 2  (envs/vss.py:343)      */
 #define O_FIELD_HY 0.65f      /* field_height / 2                        */
 #define O_GOAL_HY 0.2f        /* goal_height / 2  (envs/vss.py:344)      */
@@ -34,9 +34,9 @@
 #define O_WHEEL_R 0.024f      /* envs/vss.py:401                         */
 #define O_HALF_TRACK 0.03375f /* envs/vss_robot.urdf:54,62               */
 #define O_INV_TRACK 14.814815f
-#define O_DV 0.075f           /* wheel traction accel 6 m/s^2 * H        */
-#define O_DL 0.0858375f       /* lateral friction accel 0.7*9.81 * H     */
-#define O_K_BALL 0.998125f    /* ball rolling damping 0.15/s over H      */
+#define O_DV 0.15f            /* wheel traction accel 6 m/s^2 * H        */
+#define O_DL 0.171675f        /* lateral friction accel 0.7*9.81 * H     */
+#define O_K_BALL 0.99625f     /* ball rolling damping 0.15/s over H      */
 #define O_W_ROBOT_BR 0.09465021f /* m_ball / (m_ball + m_robot) */
 #define O_W_BALL_BR 0.90534979f  /* m_robot / (m_ball + m_robot) */
 
@@ -85,6 +85,7 @@ static void sincos_poly(float r, float* s, float* c) {
 
 /* sin/cos of x for |x| <= ~3pi/4 (half-angles and small rotation steps). */
 void oracle_sincosf(float x, float* s, float* c) {
+  if (fabsf(x) < 0.78f) { sincos_poly(x, s, c); return; } /* no reduction needed */
   int k = (int)(x * 0.63661977f + (x >= 0.0f ? 0.5f : -0.5f));
   float kf = (float)k;
   float r = (x - kf * 1.5707964f) - kf * (-4.3711390e-8f);

@@ -27,9 +27,9 @@ constexpr int kWave = 64;
 constexpr int kRec = 59;  // LDS floats per field record (58 used, odd stride: no bank conflicts)
 
 // ---- model constants (reference values cited in oracle/vss_oracle.c) --------
-constexpr int NSUB = 4;
-#define K_H 0.0125f
-#define K_HH 0.00625f
+constexpr int NSUB = 2;  // Isaac Gym's default substeps per control step
+#define K_H 0.025f
+#define K_HH 0.0125f
 #define K_FIELD_HX 0.75f
 #define K_FIELD_HY 0.65f
 #define K_GOAL_HY 0.2f
@@ -44,9 +44,9 @@ constexpr int NSUB = 4;
 #define K_WHEEL_R 0.024f
 #define K_HALF_TRACK 0.03375f
 #define K_INV_TRACK 14.814815f
-#define K_DV 0.075f
-#define K_DL 0.0858375f
-#define K_BALL_DAMP 0.998125f
+#define K_DV 0.15f
+#define K_DL 0.171675f
+#define K_BALL_DAMP 0.99625f
 #define K_W_ROBOT_BR 0.09465021f
 #define K_W_BALL_BR 0.90534979f
 #define K_MIN_DIST 0.07f
@@ -118,6 +118,10 @@ __device__ __forceinline__ void sincos_poly(float r, float& s, float& c) {
 }
 
 __device__ __forceinline__ void sincos_small(float x, float& s, float& c) {
+  if (fabsf(x) < 0.78f) {  // |x| < pi/4: no reduction (always the case for yaw steps)
+    sincos_poly(x, s, c);
+    return;
+  }
   int k = (int)(x * 0.63661977f + (x >= 0.0f ? 0.5f : -0.5f));
   float kf = (float)k;
   float r = (x - kf * 1.5707964f) - kf * (-4.3711390e-8f);
@@ -222,39 +226,43 @@ __device__ __forceinline__ void contact_ball_robot(Bodies& b, int i) {
 }
 
 // Disc of radius r against the field walls (envs/vss.py:449-518), folded into x, y >= 0.
+// Face contacts are select-based (no divergent branches); only the goal-post corner, which needs
+// sqrt/div, branches.  Identical results to the branchy form in oracle/vss_oracle.c.
+__device__ __forceinline__ void push_face(float& a, float& va, float pen) {
+  const bool hit = pen > 0.0f;
+  a = hit ? a - pen : a;
+  va = (hit && va > 0.0f) ? 0.0f : va;
+}
+
 __device__ __forceinline__ void contact_walls(float& x, float& y, float& vx, float& vy, float r) {
   float sx = x < 0.0f ? -1.0f : 1.0f, sy = y < 0.0f ? -1.0f : 1.0f;
   float ax = fabsf(x), ay = fabsf(y);
   float avx = vx * sx, avy = vy * sy;
-  if (ax <= K_FIELD_HX) {
-    if (ay <= K_GOAL_HY) {
-      float dx = ax - K_FIELD_HX, dy = ay - K_GOAL_HY;
-      float d2 = dx * dx + dy * dy;
-      if (d2 < r * r) {
-        float d = sqrtf(d2);
-        float nx = -1.0f, ny = 0.0f;
-        if (d > 1e-9f) { float inv = 1.0f / d; nx = dx * inv; ny = dy * inv; }
-        float pen = r - d;
-        ax = ax + nx * pen; ay = ay + ny * pen;
-        float vn = avx * nx + avy * ny;
-        if (vn < 0.0f) { avx = avx - nx * vn; avy = avy - ny * vn; }
-      }
-    } else {
-      float pen = ax + r - K_FIELD_HX;
-      if (pen > 0.0f) { ax = ax - pen; if (avx > 0.0f) avx = 0.0f; }
+  const bool in_x = ax <= K_FIELD_HX, in_y = ay <= K_GOAL_HY;
+  if (in_x && in_y) {  // near the goal-post corner (0.75, 0.2)
+    float dx = ax - K_FIELD_HX, dy = ay - K_GOAL_HY;
+    float d2 = dx * dx + dy * dy;
+    if (d2 < r * r) {
+      float d = sqrtf(d2);
+      float nx = -1.0f, ny = 0.0f;
+      if (d > 1e-9f) { float inv = 1.0f / d; nx = dx * inv; ny = dy * inv; }
+      float pen = r - d;
+      ax = ax + nx * pen; ay = ay + ny * pen;
+      float vn = avx * nx + avy * ny;
+      if (vn < 0.0f) { avx = avx - nx * vn; avy = avy - ny * vn; }
     }
   } else {
-    if (ay <= K_GOAL_HY) {
-      float pen = ay + r - K_GOAL_HY;
-      if (pen > 0.0f) { ay = ay - pen; if (avy > 0.0f) avy = 0.0f; }
-    } else {
-      float px = ax - K_FIELD_HX + r, py = ay - K_GOAL_HY + r;
-      if (px < py) { ax = ax - px; if (avx > 0.0f) avx = 0.0f; }
-      else { ay = ay - py; if (avy > 0.0f) avy = 0.0f; }
-    }
+    // end-wall face (in_x, !in_y), goal-pocket side face (!in_x, in_y), or centre inside the
+    // end wall (!in_x, !in_y): shortest way out
+    const float px = ax - K_FIELD_HX + r, py = ay - K_GOAL_HY + r;
+    const float pen_end = ax + r - K_FIELD_HX, pen_side = ay + r - K_GOAL_HY;
+    const bool use_x = in_x || (!in_y && px < py);
+    const float pen = in_x ? pen_end : (in_y ? pen_side : (px < py ? px : py));
+    push_face(ax, avx, use_x ? pen : -1.0f);
+    push_face(ay, avy, use_x ? -1.0f : pen);
   }
-  { float pen = ay + r - K_FIELD_HY; if (pen > 0.0f) { ay = ay - pen; if (avy > 0.0f) avy = 0.0f; } }
-  { float pen = ax + r - K_GOAL_BACK_X; if (pen > 0.0f) { ax = ax - pen; if (avx > 0.0f) avx = 0.0f; } }
+  push_face(ay, avy, ay + r - K_FIELD_HY);
+  push_face(ax, avx, ax + r - K_GOAL_BACK_X);
   x = ax * sx; y = ay * sy; vx = avx * sx; vy = avy * sy;
 }
 

@@ -17,7 +17,12 @@ from vss_amd import _native as N  # noqa: E402
 
 VARIANTS = {"full": [], "no_physics": ["-DVSS_PROF_SKIP_PHYSICS"], "no_obs": ["-DVSS_PROF_SKIP_OBS"],
             "no_physics_no_obs": ["-DVSS_PROF_SKIP_PHYSICS", "-DVSS_PROF_SKIP_OBS"]}
-EXTRA = [v for v in os.environ.get("ABLATE_EXTRA", "").split(",") if v]
+# extra variants: ABLATE_EXTRA="name=flag flag;name2=flag"
+for item in [v for v in os.environ.get("ABLATE_EXTRA", "").split(";") if v]:
+    k, _, flags = item.partition("=")
+    VARIANTS[k] = flags.split()
+VARIANTS = {k: v for k, v in VARIANTS.items()
+            if os.path.exists(os.path.join(REPO, "tools", "_build", f"libvss_{k}.so")) or len(sys.argv) > 1}
 
 
 def build(name, flags):
@@ -44,7 +49,9 @@ def main():
     io = N.VssStepIO(acts.data_ptr(), None, env.obs_buf.data_ptr(), env.terminal_obs_buf.data_ptr(),
                      env.rew_buf.data_ptr(), None, None, env.timeout_buf.data_ptr(), env.progress_f_buf.data_ptr())
     stream = N.stream_of(env.device)
-    for name in VARIANTS:
+    import glob
+    names = sorted(os.path.basename(p)[7:-3] for p in glob.glob(os.path.join(REPO, "tools", "_build", "libvss_*.so")))
+    for name in names:
         path = os.path.join(REPO, "tools", "_build", f"libvss_{name}.so")
         L = ctypes.CDLL(path)
         L.vss_step.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32] + [ctypes.c_void_p] * 3

@@ -57,7 +57,7 @@ def parse():
     p.add_argument("--mode", default="full", choices=["full", "sa", "cma", "dma"])
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--graph", type=int, default=1, help="replay the launches from a HIP graph (1) or launch eagerly (0)")
+    p.add_argument("--graph", type=int, default=0, help="replay the launches from a HIP graph (1) or launch eagerly (0)")
     return p.parse_args()
 
 
@@ -156,8 +156,6 @@ def main():
                 rc = lib.vss_step(cap_stream, n, mode, byref(prm), byref(st), byref(cios[k]))
                 if rc:
                     N.check(rc, "vss_step (capture)")
-        if args.steps % len(cios):
-            raise SystemExit(f"--graph needs --steps to be a multiple of {len(cios)}")
         graph.replay()
         torch.cuda.synchronize()
 
@@ -169,6 +167,8 @@ def main():
     if graph is not None:
         for _ in range(args.steps // len(cios)):
             graph.replay()
+        for k in range(args.steps % len(cios)):  # remainder launched eagerly, same stream
+            launch(k)
     else:
         for k in range(args.steps):
             launch(k)

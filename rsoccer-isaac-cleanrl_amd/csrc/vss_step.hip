@@ -489,6 +489,17 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
   float* rec = lds + lane * kRec;
 
+  // -- state loads first (46 coalesced channel loads in flight), then the action transpose -------
+  int64_t progress = 0, reset_prev = 0;
+  uint32_t ctr = 0;
+  Bodies b = {};
+  if (valid) {
+    progress = args.s.progress_buf[f];
+    reset_prev = args.s.reset_buf[f];
+    ctr = args.s.rng_counter[f];
+    load_bodies(args.s.state, n, f, b);
+  }
+
   // -- actions: FULL reads (N,12); wrapped modes read + update the OU action buffer --------------
   float a[12];
   if constexpr (MODE == VSS_MODE_FULL) {
@@ -500,16 +511,6 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
 #pragma unroll
   for (int k = 0; k < 12; ++k) a[k] = rec[k];
   __syncthreads();
-
-  int64_t progress = 0, reset_prev = 0;
-  uint32_t ctr = 0;
-  Bodies b = {};
-  if (valid) {
-    progress = args.s.progress_buf[f];
-    reset_prev = args.s.reset_buf[f];
-    ctr = args.s.rng_counter[f];
-    load_bodies(args.s.state, n, f, b);
-  }
 
   if constexpr (MODE != VSS_MODE_FULL) {
     // random_ou (envs/wrappers.py:5-19): a <- clamp(a - 0.1 a + N(0, 0.15^2), -1, 1); the learner

@@ -25,8 +25,9 @@ run() {  # run <name> <seconds> <cmd...>
 
 STEPS=${STEPS:-tests,smoke,bench,prof}
 case ",$STEPS," in *,tests,*) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;; esac
+case ",$STEPS," in *,tplay,*) run pytest_play 600 python -m pytest tests/test_play.py -m gpu -x -q ;; esac
 case ",$STEPS," in *,smoke,*) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;; esac
-case ",$STEPS," in *,bench,*) run bench 400 python bench.py ;; esac
+case ",$STEPS," in *,bench,*) run bench 400 python bench.py; run bench_eager 300 python bench.py --graph 0 --no-cpu-baseline ;; esac
 case ",$STEPS," in *,benchsa,*) run bench_sa 300 python bench.py --mode sa --no-cpu-baseline ;; esac
 case ",$STEPS," in *,prof,*)
   run rocprof_stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \

@@ -57,6 +57,9 @@ def parse():
     p.add_argument("--mode", default="full", choices=["full", "sa", "cma", "dma"])
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="nccl (= RCCL) for real multi-GPU runs; gloo + --share-gpu to rehearse ranks on one GPU")
+    p.add_argument("--share-gpu", action="store_true", help="map every rank to cuda:0 (rehearsal only)")
     p.add_argument("--graph", type=int, default=0, help="replay the launches from a HIP graph (1) or launch eagerly (0)")
     return p.parse_args()
 
@@ -83,6 +86,14 @@ def cpu_baseline(seconds: float):
                       f"random actions, 1 thread, host CPU: {cpu_model()}"}
 
 
+def reduce_max(values, device="cpu"):
+    """Max over ranks of the per-rank timings (the only cross-rank data besides barriers)."""
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.cpu()]
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -98,9 +109,12 @@ def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.dist_backend == "nccl":  # RCCL on ROCm
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(args.dist_backend)
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
 
@@ -188,10 +202,7 @@ def main():
     torch.cuda.synchronize()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms = reduce_max([elapsed, kern_ms], dev if args.dist_backend == "nccl" else "cpu")
 
     if rank == 0:
         agents = 3 if args.mode == "dma" else 1

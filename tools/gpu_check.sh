@@ -41,4 +41,10 @@ case ",$STEPS," in *,pmc,*)
 esac
  case ",$STEPS," in *,ablate,*) run ablate 300 python tools/ablate.py ;; esac
 case ",$STEPS," in *,ppo,*) run ppo_sa 900 python rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 2 --save-path /tmp/runs ;; esac
+case ",$STEPS," in *,sq,*)
+  run rocprof_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY --output-format csv -d "$OUT/pmc_sq_$TAG" -o run -- \
+      python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline
+  run rocprof_sq2 400 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM_WR SQ_INSTS_SMEM GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_sq2_$TAG" -o run -- \
+      python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+esac
 echo "session done" | tee -a "$OUT/session.log"

@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--mode", default="full", choices=["full", "sa", "cma", "dma"])
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--ppo-updates", type=int, default=None,
+                   help="PPO training updates timed after the env-step benchmark (default: 2 at N=1, 0 otherwise)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL) for real multi-GPU runs; gloo + --share-gpu to rehearse ranks on one GPU")
     p.add_argument("--share-gpu", action="store_true", help="map every rank to cuda:0 (rehearsal only)")
@@ -84,6 +86,27 @@ def cpu_baseline(seconds: float):
     return {"value": n * steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
             "sample": f"oracle/vss_oracle.c FULL contract, {n} fields x {steps} steps ({el:.1f} s), "
                       f"random actions, 1 thread, host CPU: {cpu_model()}"}
+
+
+def ppo_wallclock(n_envs: int, updates: int, dev) -> dict:
+    """The full SA PPO loop (ppo_continuous_action_isaacgym.py, reference defaults: T=128,
+    8 epochs x 4 minibatches, fp32) at `n_envs` envs; the last update is timed and projected to
+    1e8 env-steps (ceil(1e8 / batch) updates; the reference's floor-division gives one fewer)."""
+    import math
+    import ppo_continuous_action_isaacgym as P
+    args = P.parse_args(["--env-id", "sa", "--num-envs", str(n_envs), "--num-updates", str(updates),
+                         "--log", "false", "--seed", "1"])
+    _, hist = P.train(args)
+    last = hist[-1]
+    per_update = last["rollout_s"] + last["update_s"]
+    batch = args.batch_size
+    updates_1e8 = math.ceil(1e8 / batch)
+    return {"env": "sa", "num_envs": n_envs, "num_steps": args.num_steps, "batch": batch,
+            "update_epochs": args.update_epochs, "num_minibatches": args.num_minibatches, "dtype": "f32",
+            "rollout_s": last["rollout_s"], "update_s": last["update_s"],
+            "rollout_env_steps_per_s": batch / last["rollout_s"], "train_env_steps_per_s": batch / per_update,
+            "wallclock_to_1e8_steps_s": updates_1e8 * per_update, "updates_to_1e8": updates_1e8,
+            "timed_update": len(hist)}
 
 
 def reduce_max(values, device="cpu"):
@@ -240,6 +263,9 @@ def main():
                          "frac": achieved / HBM_PEAK, "traffic": traffic,
                          "algorithmic_bytes_per_launch": algo, "kernel_ms": kern_ms},
         }
+        ppo_updates = args.ppo_updates if args.ppo_updates is not None else (2 if world == 1 else 0)
+        if ppo_updates > 0:
+            out["ppo"] = ppo_wallclock(n, ppo_updates, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -81,6 +81,8 @@ def parse_args(argv=None):
     p.add_argument("--save-path", type=str, default="runs")
     p.add_argument("--num-updates", type=int, default=None, help="override total_timesteps // batch")
     p.add_argument("--log", type=b, default=True, nargs="?", const=True)
+    p.add_argument("--amp", type=str, default="none", choices=["none", "bf16"],
+                   help="bf16 autocast for the MLP GEMMs (off = the reference's fp32 numerics)")
     args = p.parse_args(argv)
     args.batch_size = int(args.num_envs * args.num_steps)
     args.minibatch_size = int(args.batch_size // args.num_minibatches)
@@ -187,6 +189,12 @@ def compute_gae(rewards, values, next_values, next_dones, next_timeouts, gamma, 
     return advantages, advantages + values
 
 
+def autocast(args, device):
+    """bf16 autocast for the MLP GEMMs when --amp bf16 (fp32 master weights, fp32 losses)."""
+    enabled = getattr(args, "amp", "none") == "bf16" and torch.device(device).type == "cuda"
+    return torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=enabled)
+
+
 def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_advantages, b_returns,
                b_values, world=1, gen=None):
     """Clipped PPO over update_epochs x num_minibatches (ppo…:306-365).  Returns last-minibatch
@@ -200,7 +208,9 @@ def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_adv
         b_inds = torch.randperm(batch, device=device, generator=gen)
         for start in range(0, batch, mb):
             mb_inds = b_inds[start:start + mb]
-            _, newlogprob, entropy, newvalue = agent.get_action_and_value(b_obs[mb_inds], b_actions[mb_inds])
+            with autocast(args, device):
+                _, newlogprob, entropy, newvalue = agent.get_action_and_value(b_obs[mb_inds], b_actions[mb_inds])
+            newlogprob, entropy, newvalue = newlogprob.float(), entropy.float(), newvalue.float()
             logratio = newlogprob - b_logprobs[mb_inds]
             ratio = logratio.exp()
             with torch.no_grad():
@@ -311,15 +321,15 @@ def train(args):
         for step in range(T):
             global_step += E * world
             obs[step] = next_obs
-            with torch.no_grad():
+            with torch.no_grad(), autocast(args, device):
                 action, logprob, _, value = agent.get_action_and_value(next_obs)
                 values[step] = value.flatten()
-            actions[step] = action
-            logprobs[step] = logprob
+            actions[step] = action.float()
+            logprobs[step] = logprob.float()
             next_obs, rewards[step], next_done, info = envs.step(action)
             next_dones[step] = next_done
             next_timeouts[step] = info["time_outs"]
-            with torch.no_grad():
+            with torch.no_grad(), autocast(args, device):
                 next_values[step] = agent.get_value(info["terminal_observation"]).reshape(1, -1)
             d = next_done.float()
             ep_ret += (info["r"]["return"] * d).sum()

@@ -64,3 +64,13 @@ def test_product_path_refuses_cpu():
     from envs.vss import VSS, default_cfg
     with pytest.raises(N.NativeError):
         VSS(default_cfg(16), "cpu", "cpu", 0, True, False, False)
+
+
+def test_oracle_under_asan_ubsan():
+    """The CPU restatement driven through every mode / size under ASan + UBSan (host sanitizers;
+    GPU sanitizers are not available on the MI355X pool)."""
+    import subprocess
+    r = subprocess.run(["make", "-s", "-C", os.path.join(os.path.dirname(N.HEADER), "..", "oracle"), "check-asan"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "oracle selftest ok" in r.stdout

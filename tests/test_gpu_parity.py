@@ -223,3 +223,45 @@ def test_ou_noise_statistics():
     assert abs(z.mean()) < 2e-3 and abs(z.std() - 0.15) < 2e-3
     # 4th moment of a normal: 3 sigma^4
     assert abs((z ** 4).mean() / 0.15 ** 4 - 3.0) < 0.1
+
+
+def test_graph_replay_matches_eager():
+    """vss_step captured into a hipGraph and replayed gives the same bits as eager launches (the
+    per-field RNG counters live in device memory, so replays draw fresh randoms)."""
+    n = 4096
+    e1, e2 = make_vss(n, max_len=25, seed=3), make_vss(n, max_len=25, seed=3)
+    acts = [torch.rand((n, 12), device=DEV) * 2 - 1 for _ in range(4)]
+    lib = N.load()
+    io2 = N.VssStepIO(0, None, e2.obs_buf.data_ptr(), e2.terminal_obs_buf.data_ptr(), e2.rew_buf.data_ptr(), None,
+                      None, e2.timeout_buf.data_ptr(), e2.progress_f_buf.data_ptr())
+    prm, st = e2._c_params(), e2._c_state()
+    ios = []
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.graph(g, stream=s):
+        for a in acts:
+            io = N.VssStepIO.from_buffer_copy(io2)
+            io.actions = a.data_ptr()
+            ios.append(io)
+            assert lib.vss_step(N.stream_of(torch.device(DEV)), n, 0, N.ctypes.byref(prm), N.ctypes.byref(st),
+                                N.ctypes.byref(io)) == 0
+    for rep in range(15):  # 60 steps: crosses two time-out waves (max_len 25)
+        g.replay()
+        for a in acts:
+            e1.step(a)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.state, e2.state)
+    assert torch.equal(e1.obs_buf, e2.obs_buf) and torch.equal(e1.rew_buf, e2.rew_buf)
+    assert torch.equal(e1.progress_buf, e2.progress_buf) and torch.equal(e1.rng_counter, e2.rng_counter)
+
+
+def test_zero_fields_is_a_noop():
+    lib = N.load()
+    env = make_vss(4)
+    prm, st = env._c_params(), env._c_state()
+    io = N.VssStepIO(env.obs_buf.data_ptr(), None, env.obs_buf.data_ptr(), env.terminal_obs_buf.data_ptr(),
+                     env.rew_buf.data_ptr(), None, None, env.timeout_buf.data_ptr(), env.progress_f_buf.data_ptr())
+    before = env.state.clone()
+    assert lib.vss_step(N.stream_of(env.device), 0, 0, N.ctypes.byref(prm), N.ctypes.byref(st), N.ctypes.byref(io)) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(before, env.state)

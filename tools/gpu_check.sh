@@ -40,6 +40,11 @@ case ",$STEPS," in *,pmc,*)
       python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
 esac
  case ",$STEPS," in *,ablate,*) run ablate 300 python tools/ablate.py ;; esac
+case ",$STEPS," in *,amp,*) run ppo_amp 900 python rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 2 --amp bf16 --save-path /tmp/runs ;; esac
+case ",$STEPS," in *,ppoprof,*)
+  run rocprof_ppo 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_ppo_$TAG" -o run -- \
+      python3 rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 1 --log false ;;
+esac
 case ",$STEPS," in *,ppo,*) run ppo_sa 900 python rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 2 --save-path /tmp/runs ;; esac
 case ",$STEPS," in *,sq,*)
   run rocprof_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY --output-format csv -d "$OUT/pmc_sq_$TAG" -o run -- \

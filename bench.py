@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--mode", default="full", choices=["full", "sa", "cma", "dma"])
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--rollout-k", type=int, default=16,
+                   help="also time vss_rollout with K steps per launch (0 = skip)")
     p.add_argument("--ppo-updates", type=int, default=None,
                    help="PPO training updates timed after the env-step benchmark (default: 2 at N=1, 0 otherwise)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -86,6 +88,35 @@ def cpu_baseline(seconds: float):
     return {"value": n * steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
             "sample": f"oracle/vss_oracle.c FULL contract, {n} fields x {steps} steps ({el:.1f} s), "
                       f"random actions, 1 thread, host CPU: {cpu_model()}"}
+
+
+def rollout_leg(env, K: int, steps: int, gen, dev) -> dict:
+    """vss_rollout: K FULL steps per launch for a pre-supplied random action sequence (the
+    open-loop form of the same workload; state on chip between steps).  Bytes per field-step:
+    actions 48 + obs 1248 + terminal obs 1248 + rew 96 + done 8 + time-out 1 + progress 4, plus
+    the state / bookkeeping / dof read+write (456 B) once per launch."""
+    n = env.num_fields
+    acts = torch.rand((K, n, 2, 3, 2), device=dev, generator=gen) * 2 - 1
+    out = env.rollout(acts)
+    env.rollout(acts, out)
+    torch.cuda.synchronize()
+    launches = max(1, steps // K)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(launches):
+        env.rollout(acts, out)
+    e1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    launch_ms = e0.elapsed_time(e1) / launches
+    per_step_bytes = 48 + 1248 + 1248 + 96 + 8 + 1 + 4
+    algo = n * (K * per_step_bytes + 368 + 32 + 8 + 48)
+    achieved = algo / (launch_ms * 1e-3)
+    return {"steps_per_launch": K, "launches": launches, "value": n * K * launches / wall, "unit": "env-steps/s",
+            "ms_per_step": launch_ms / K,
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": algo, "kernel_ms": launch_ms}}
 
 
 def ppo_wallclock(n_envs: int, updates: int, dev) -> dict:
@@ -263,6 +294,8 @@ def main():
                          "frac": achieved / HBM_PEAK, "traffic": traffic,
                          "algorithmic_bytes_per_launch": algo, "kernel_ms": kern_ms},
         }
+        if args.rollout_k > 0 and mode == N.MODE_FULL:
+            out["rollout"] = rollout_leg(env, args.rollout_k, args.steps, gen, dev)
         ppo_updates = args.ppo_updates if args.ppo_updates is not None else (2 if world == 1 else 0)
         if ppo_updates > 0:
             out["ppo"] = ppo_wallclock(n, ppo_updates, dev)

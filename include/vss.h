@@ -109,6 +109,23 @@ typedef struct vss_step_io {
   float* progress_f;
 } vss_step_io;
 
+/*
+ * Open-loop rollout buffers for vss_rollout (K = n_steps, N = n_fields), step-major:
+ *   actions      (K,N,2,3,2) fp32                                                   read
+ *   obs          (K,N,2,3,52), terminal_obs (K,N,2,3,52), rew (K,N,2,3,4) fp32      write
+ *   dones        (K,N) int64 = reset_buf after each step                            write
+ *   time_outs    (K,N) uint8, progress_f (K,N) fp32                                 write
+ */
+typedef struct vss_rollout_io {
+  const float* actions;
+  float* obs;
+  float* terminal_obs;
+  float* rew;
+  int64_t* dones;
+  uint8_t* time_outs;
+  float* progress_f;
+} vss_rollout_io;
+
 /* ABI version (VSS_ABI_VERSION). */
 int vss_abi_version(void);
 
@@ -123,6 +140,15 @@ const char* vss_error_string(int code);
  */
 int vss_step(void* stream, int64_t n_fields, int32_t mode, const vss_params* params,
              const vss_state* st, const vss_step_io* io);
+
+/*
+ * K consecutive FULL-mode steps in one launch for a pre-supplied action sequence (random-action
+ * benchmarks, scripted / OU opponents, evaluation): bit-identical to K vss_step(FULL) calls — the
+ * same reference semantics per step (envs/vss.py:180-333) — with the field state kept on chip
+ * between steps.  State buffers (st) are updated as after the K-th step.
+ */
+int vss_rollout(void* stream, int64_t n_fields, int32_t n_steps, const vss_params* params,
+                const vss_state* st, const vss_rollout_io* io);
 
 /*
  * Re-sample every field whose reset_buf != 0 (VSS.reset_dones, envs/vss.py:267-333);

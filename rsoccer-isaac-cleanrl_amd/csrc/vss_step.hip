@@ -465,6 +465,41 @@ __device__ __forceinline__ void reset_field(Bodies& b, uint32_t k0, uint32_t k1,
   b.bvy = u01(o[7]) - 0.5f;
 }
 
+// ---- rewards and dones (compute_rewards_and_dones, envs/vss.py:218-265, 578-655) --------------------
+// (pbx, pby, prx, pry): positions before the physics; `a`: the clamped actions (= dof_velocity_buf).
+__device__ __forceinline__ int64_t rewards_and_done(const vss_params& p, const Bodies& b, float pbx, float pby,
+                                                   const float prx[6], const float pry[6], const float a[12],
+                                                   int64_t progress, float rew[24]) {
+  const float bx = b.bx, by = b.by;
+  const bool is_goal = (fabsf(bx) > K_FIELD_HX) && (fabsf(by) < K_GOAL_HY);
+  const float g = is_goal ? (bx > 0.0f ? 1.0f : (bx < 0.0f ? -1.0f : 0.0f)) : 0.0f;
+  float grad;
+  {
+    float lx = bx - (-K_FIELD_HX), ly = by - (-0.0f), rx = bx - K_FIELD_HX, ry = by - 0.0f;
+    float pot = sqrtf(lx * lx + ly * ly) - sqrtf(rx * rx + ry * ry);
+    float plx = pbx - (-K_FIELD_HX), ply = pby - (-0.0f), prx_ = pbx - K_FIELD_HX, pry_ = pby - 0.0f;
+    float ppot = sqrtf(plx * plx + ply * ply) - sqrtf(prx_ * prx_ + pry_ * pry_);
+    grad = pot - ppot;
+  }
+#pragma unroll
+  for (int ag = 0; ag < 6; ++ag) {
+    const bool blue = ag < 3;
+    float r0 = 0.0f, r1 = 0.0f, r2 = 0.0f, r3 = 0.0f;
+    if (p.w_goal > 0.0f) r0 = (blue ? g : (0.0f - g)) * p.w_goal;
+    if (p.w_grad > 0.0f) r1 = (blue ? grad : -grad) * p.w_grad;
+    if (p.w_move > 0.0f) {
+      float dx0 = prx[ag] - pbx, dy0 = pry[ag] - pby;
+      float dx1 = b.x[ag] - bx, dy1 = b.y[ag] - by;
+      float pd = sqrtf(dx0 * dx0 + dy0 * dy0), d = sqrtf(dx1 * dx1 + dy1 * dy1);
+      r2 = 0.0f + (pd - d) * p.w_move;
+    }
+    if (p.w_energy > 0.0f)
+      r3 = 0.0f + (-((fabsf(a[2 * ag]) + fabsf(a[2 * ag + 1])) / 2.0f)) * p.w_energy;
+    rew[4 * ag] = r0; rew[4 * ag + 1] = r1; rew[4 * ag + 2] = r2; rew[4 * ag + 3] = r3;
+  }
+  return (is_goal || progress >= (int64_t)p.max_episode_length) ? 1 : 0;
+}
+
 // ---- the step kernel -------------------------------------------------------------------------------
 struct StepArgs {
   int64_t n;
@@ -562,35 +597,8 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
 
   // -- post_physics_step: progress, rewards, dones (envs/vss.py:189-265) ----------------------------------
   progress += 1;
-  const float bx = b.bx, by = b.by;
-  const bool is_goal = (fabsf(bx) > K_FIELD_HX) && (fabsf(by) < K_GOAL_HY);
-  const float g = is_goal ? (bx > 0.0f ? 1.0f : (bx < 0.0f ? -1.0f : 0.0f)) : 0.0f;
-  float grad;
-  {
-    float lx = bx - (-K_FIELD_HX), ly = by - (-0.0f), rx = bx - K_FIELD_HX, ry = by - 0.0f;
-    float pot = sqrtf(lx * lx + ly * ly) - sqrtf(rx * rx + ry * ry);
-    float plx = pbx - (-K_FIELD_HX), ply = pby - (-0.0f), prx_ = pbx - K_FIELD_HX, pry_ = pby - 0.0f;
-    float ppot = sqrtf(plx * plx + ply * ply) - sqrtf(prx_ * prx_ + pry_ * pry_);
-    grad = pot - ppot;
-  }
   float rew[24];
-#pragma unroll
-  for (int ag = 0; ag < 6; ++ag) {
-    const bool blue = ag < 3;
-    float r0 = 0.0f, r1 = 0.0f, r2 = 0.0f, r3 = 0.0f;
-    if (args.p.w_goal > 0.0f) r0 = (blue ? g : (0.0f - g)) * args.p.w_goal;
-    if (args.p.w_grad > 0.0f) r1 = (blue ? grad : -grad) * args.p.w_grad;
-    if (args.p.w_move > 0.0f) {
-      float dx0 = prx[ag] - pbx, dy0 = pry[ag] - pby;
-      float dx1 = b.x[ag] - bx, dy1 = b.y[ag] - by;
-      float pd = sqrtf(dx0 * dx0 + dy0 * dy0), d = sqrtf(dx1 * dx1 + dy1 * dy1);
-      r2 = 0.0f + (pd - d) * args.p.w_move;
-    }
-    if (args.p.w_energy > 0.0f)
-      r3 = 0.0f + (-((fabsf(a[2 * ag]) + fabsf(a[2 * ag + 1])) / 2.0f)) * args.p.w_energy;
-    rew[4 * ag] = r0; rew[4 * ag + 1] = r1; rew[4 * ag + 2] = r2; rew[4 * ag + 3] = r3;
-  }
-  const int64_t done = (is_goal || progress >= (int64_t)args.p.max_episode_length) ? 1 : 0;
+  const int64_t done = rewards_and_done(args.p, b, pbx, pby, prx, pry, a, progress, rew);
 
   // -- terminal observation (envs/vss.py:195-196) ----------------------------------------------------------
   write_obs_record(rec, b, a);
@@ -683,6 +691,125 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   }
 }
 
+// ---- K control steps per launch (open-loop action sequences) -----------------------------------------
+// Same per-step semantics as K consecutive step_kernel<FULL> launches, bit for bit (the Philox
+// counter of step k is rng_counter + k), but the field state stays in registers across steps, each
+// step's observation stores drain while the next step's physics runs, and the next step's actions
+// are prefetched into registers before the current step's streams are issued.
+struct RolloutArgs {
+  int64_t n;
+  int32_t k_steps;
+  vss_params p;
+  vss_state s;
+  vss_rollout_io io;
+};
+
+__device__ __forceinline__ void prefetch12(const float* __restrict__ g, int nv, int lane, float4 pre[3]) {
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int q = lane + j * kWave;
+    if (q < nv * 3) pre[j] = g4[q];
+  }
+}
+
+__device__ __forceinline__ void stage12(const float4 pre[3], int nv, float* lds, int lane) {
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int q = lane + j * kWave;
+    if (q < nv * 3) {
+      const int fl = q / 3, k = (q - fl * 3) * 4;
+      float* d = lds + fl * kRec + k;
+      d[0] = pre[j].x; d[1] = pre[j].y; d[2] = pre[j].z; d[3] = pre[j].w;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
+  __shared__ float lds[kWave * kRec];
+  const int64_t n = args.n;
+  const int lane = threadIdx.x;
+  const int64_t f0 = (int64_t)blockIdx.x * kWave;
+  const int nv = (int)(n - f0 < kWave ? n - f0 : kWave);
+  const int64_t f = f0 + lane;
+  const bool valid = lane < nv;
+  const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
+  float* rec = lds + lane * kRec;
+
+  int64_t progress = 0, reset_prev = 0;
+  uint32_t ctr = 0;
+  Bodies b = {};
+  if (valid) {
+    progress = args.s.progress_buf[f];
+    reset_prev = args.s.reset_buf[f];
+    ctr = args.s.rng_counter[f];
+    load_bodies(args.s.state, n, f, b);
+  }
+  float4 pre[3];
+  prefetch12(args.io.actions + f0 * 12, nv, lane, pre);
+  float dof[12];
+  int64_t done = reset_prev;
+  const float clip = args.p.clip_actions;
+
+  for (int k = 0; k < args.k_steps; ++k) {
+    const int64_t step_off = (int64_t)k * n;
+    float a[12];
+    stage12(pre, nv, lds, lane);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 12; ++i) a[i] = clampf(rec[i], -clip, clip);
+    __syncthreads();
+    if (k + 1 < args.k_steps) prefetch12(args.io.actions + (step_off + n + f0) * 12, nv, lane, pre);
+
+    if (reset_prev != 0) progress = 0;
+    float pbx = b.bx, pby = b.by, prx[6], pry[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) { prx[i] = b.x[i]; pry[i] = b.y[i]; }
+    if (valid) physics(b, a);
+    progress += 1;
+    float rew[24];
+    done = rewards_and_done(args.p, b, pbx, pby, prx, pry, a, progress, rew);
+
+    write_obs_record(rec, b, a);
+    __syncthreads();
+    coop_store_obs<6>(args.io.terminal_obs + (step_off + f0) * 312, nv, lds, lane);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 12; ++i) dof[i] = a[i];
+    if (valid && done) {
+      reset_field(b, k0, k1, (uint32_t)f, ctr + (uint32_t)k, 0u);
+#pragma unroll
+      for (int i = 0; i < 12; ++i) dof[i] = dof[i] * 0.0f;
+    }
+    write_obs_record(rec, b, dof);
+    __syncthreads();
+    coop_store_obs<6>(args.io.obs + (step_off + f0) * 312, nv, lds, lane);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 24; ++i) rec[i] = rew[i];
+    __syncthreads();
+    coop_store<24>(args.io.rew + (step_off + f0) * 24, nv, lds, lane);
+    __syncthreads();
+    if (valid) {
+      args.io.dones[step_off + f] = done;
+      args.io.time_outs[step_off + f] = (progress >= (int64_t)args.p.max_episode_length - 1) && done != 0;
+      args.io.progress_f[step_off + f] = (float)progress;
+    }
+    reset_prev = done;
+  }
+
+  if (valid) {
+    store_bodies(args.s.state, n, f, b);
+    args.s.progress_buf[f] = progress;
+    args.s.reset_buf[f] = done;
+    args.s.rng_counter[f] = ctr + (uint32_t)args.k_steps;
+  }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) rec[i] = dof[i];
+  __syncthreads();
+  coop_store<12>(args.s.dof_velocity_buf + f0 * 12, nv, lds, lane);
+}
+
 // External reset_dones: fields with reset_buf != 0 are re-sampled with the EXTERNAL purpose bit
 // and their rng counter advances (so repeated calls draw afresh).  dof_velocity_buf zeroed.
 __global__ __launch_bounds__(kWave) void reset_kernel(int64_t n, vss_params p, vss_state s) {
@@ -766,6 +893,19 @@ int vss_step(void* stream, int64_t n, int32_t mode, const vss_params* p, const v
     case VSS_MODE_CMA: hipLaunchKernelGGL(vss::step_kernel<VSS_MODE_CMA>, grid, block, 0, s, args); break;
     default: hipLaunchKernelGGL(vss::step_kernel<VSS_MODE_DMA>, grid, block, 0, s, args); break;
   }
+  return launch_status();
+}
+
+int vss_rollout(void* stream, int64_t n, int32_t k_steps, const vss_params* p, const vss_state* st,
+                const vss_rollout_io* io) {
+  if (int rc = check_state(n, st)) return rc;
+  if (!p || !io || k_steps < 1 || k_steps > (1 << 20)) return VSS_E_ARG;
+  if (!io->actions || !io->obs || !io->terminal_obs || !io->rew || !io->dones || !io->time_outs || !io->progress_f)
+    return VSS_E_ARG;
+  if (n == 0) return VSS_OK;
+  vss::RolloutArgs args{n, k_steps, *p, *st, *io};
+  const dim3 grid((unsigned)((n + vss::kWave - 1) / vss::kWave)), block(vss::kWave);
+  hipLaunchKernelGGL(vss::rollout_kernel, grid, block, 0, (hipStream_t)stream, args);
   return launch_status();
 }
 

@@ -188,6 +188,34 @@ class VSS:
         self.obs_dict["obs"] = self._clipped(self.obs_buf)
         return self.obs_dict, self.rew_buf, self.reset_buf, self.extras
 
+    def rollout(self, actions: torch.Tensor, out: dict | None = None) -> dict:
+        """K FULL-mode steps of a pre-supplied action sequence `actions` (K, N, 2, 3, 2) in ONE
+        launch (vss_rollout): identical to K `step()` calls, returning per-step tensors
+        obs / terminal_observation (K,N,2,3,52), rew (K,N,2,3,4), dones (K,N) int64,
+        time_outs (K,N) bool, progress_buffer (K,N).  For open-loop rollouts (scripted or OU
+        opponents, random-action benchmarks); the env state ends as after the K-th step."""
+        K = int(actions.shape[0])
+        n = self.num_fields
+        if actions.numel() != K * n * 12:
+            raise ValueError(f"actions must be (K, {n}, 2, 3, 2), got {tuple(actions.shape)}")
+        actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        if out is None:
+            dev = self.device
+            out = dict(obs=torch.empty((K, n, 2, 3, 52), device=dev),
+                       terminal_observation=torch.empty((K, n, 2, 3, 52), device=dev),
+                       rew=torch.empty((K, n, 2, 3, 4), device=dev),
+                       dones=torch.empty((K, n), device=dev, dtype=torch.long),
+                       time_outs=torch.empty((K, n), device=dev, dtype=torch.bool),
+                       progress_buffer=torch.empty((K, n), device=dev))
+        rio = N.VssRolloutIO(actions.data_ptr(), out["obs"].data_ptr(), out["terminal_observation"].data_ptr(),
+                             out["rew"].data_ptr(), out["dones"].data_ptr(), out["time_outs"].data_ptr(),
+                             out["progress_buffer"].data_ptr())
+        prm, st = self._c_params(), self._c_state()
+        rc = N.load().vss_rollout(N.stream_of(self.device), n, K, N.ctypes.byref(prm), N.ctypes.byref(st),
+                                  N.ctypes.byref(rio))
+        N.check(rc, "vss_rollout")
+        return out
+
     def _clipped(self, obs):
         if math.isinf(self.clip_obs):
             return obs

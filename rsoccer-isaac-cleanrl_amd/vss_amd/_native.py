@@ -23,7 +23,7 @@ MODE_FULL, MODE_SA, MODE_CMA, MODE_DMA = 0, 1, 2, 3
 STATE_CHANNELS = 58
 CH_BALL_X, CH_BALL_Y, CH_BALL_VX, CH_BALL_VY = 0, 1, 2, 3
 CH_RX, CH_RY, CH_RQX, CH_RQY, CH_RQZ, CH_RQW, CH_RVX, CH_RVY, CH_RW = 4, 10, 16, 22, 28, 34, 40, 46, 52
-EXPORTED = ("vss_abi_version", "vss_error_string", "vss_step", "vss_reset_dones",
+EXPORTED = ("vss_abi_version", "vss_error_string", "vss_step", "vss_rollout", "vss_reset_dones",
             "vss_compute_observations")
 
 
@@ -50,6 +50,11 @@ class VssStepIO(ctypes.Structure):
                  "time_outs", "progress_f")]
 
 
+class VssRolloutIO(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in
+                ("actions", "obs", "terminal_obs", "rew", "dones", "time_outs", "progress_f")]
+
+
 class NativeError(RuntimeError):
     pass
 
@@ -73,6 +78,8 @@ def load() -> ctypes.CDLL:
     L.vss_error_string.restype = ctypes.c_char_p
     L.vss_step.argtypes = [P, i64, i32, P, P, P]
     L.vss_step.restype = ctypes.c_int
+    L.vss_rollout.argtypes = [P, i64, i32, P, P, P]
+    L.vss_rollout.restype = ctypes.c_int
     L.vss_reset_dones.argtypes = [P, i64, P, P]
     L.vss_reset_dones.restype = ctypes.c_int
     L.vss_compute_observations.argtypes = [P, i64, P, P, i32]

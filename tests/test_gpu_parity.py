@@ -265,3 +265,28 @@ def test_zero_fields_is_a_noop():
     assert lib.vss_step(N.stream_of(env.device), 0, 0, N.ctypes.byref(prm), N.ctypes.byref(st), N.ctypes.byref(io)) == 0
     torch.cuda.synchronize()
     assert torch.equal(before, env.state)
+
+
+@pytest.mark.parametrize("n,K", [(4096, 24), (65, 50)])
+def test_rollout_equals_sequential_steps_and_oracle(n, K):
+    """vss_rollout (K steps per launch) == K vss_step launches == K oracle steps, bit for bit."""
+    e1, e2 = make_vss(n, max_len=20, seed=11), make_vss(n, max_len=20, seed=11)
+    h = host_from(e1)
+    prm = oracle_params(e1)
+    acts = (torch.rand((K, n, 2, 3, 2), device=DEV, generator=torch.Generator(device=DEV).manual_seed(4)) * 2.6 - 1.3)
+    out = e2.rollout(acts)
+    a_np = acts.cpu().numpy()
+    for k in range(K):
+        o, r, d, x = e1.step(acts[k])
+        io = O.make_io(n, O.MODE_FULL)
+        O.step(h, O.MODE_FULL, a_np[k].reshape(n, 12), io, prm)
+        torch.cuda.synchronize()
+        assert torch.equal(out["obs"][k], o["obs"]) and torch.equal(out["terminal_observation"][k], x["terminal_observation"])
+        assert torch.equal(out["rew"][k], r) and torch.equal(out["dones"][k], d)
+        assert torch.equal(out["time_outs"][k], x["time_outs"]) and torch.equal(out["progress_buffer"][k], x["progress_buffer"])
+        np.testing.assert_array_equal(bits(out["obs"][k]).reshape(n, 312), io["obs"].view(np.uint32).reshape(n, 312))
+        np.testing.assert_array_equal(out["dones"][k].cpu().numpy(), h.reset)
+    for name in ("state", "progress_buf", "reset_buf", "dof_velocity_buf", "rng_counter"):
+        assert torch.equal(getattr(e1, name), getattr(e2, name)), name
+    assert_env_equal(e2, h, "after rollout")
+    assert int(out["dones"].sum()) > 0

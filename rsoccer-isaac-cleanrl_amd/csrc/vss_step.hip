@@ -159,6 +159,26 @@ __device__ __forceinline__ float logf_poly(float x) {
   return (float)e * 0.69314718f + s * p;
 }
 
+// ---- diagnostic-only phase stamps (tools/ablate.py builds with -DVSS_PROF_STAMPS; never in the
+// product): s_memtime deltas per physics phase, summed per wave, added to g_prof by lane 0 ----------
+#ifdef VSS_PROF_STAMPS
+__device__ unsigned long long g_prof[8];
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define PROF_DECL unsigned long long prof_t = stamp(), prof_acc[5] = {0, 0, 0, 0, 0};
+#define PROF_MARK(k) { unsigned long long t_ = stamp(); prof_acc[k] += t_ - prof_t; prof_t = t_; }
+#define PROF_FLUSH if (threadIdx.x == 0) { for (int k_ = 0; k_ < 5; ++k_) atomicAdd(&g_prof[k_], prof_acc[k_]); }
+#else
+#define PROF_DECL
+#define PROF_MARK(k)
+#define PROF_FLUSH
+#endif
+
 // ---- per-field body state in registers ---------------------------------------------------------
 struct Bodies {
   float bx, by, bvx, bvy;
@@ -267,6 +287,7 @@ __device__ __forceinline__ void contact_walls(float& x, float& y, float& vx, flo
 }
 
 __device__ __forceinline__ void physics(Bodies& b, const float a[12]) {
+  PROF_DECL
   float tl[6], tr[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
@@ -291,6 +312,7 @@ __device__ __forceinline__ void physics(Bodies& b, const float a[12]) {
       b.vx[i] = c * vf - s * vl;
       b.vy[i] = s * vf + c * vl;
     }
+    PROF_MARK(0)
     b.bvx = b.bvx * K_BALL_DAMP;
     b.bvy = b.bvy * K_BALL_DAMP;
 #pragma unroll
@@ -308,16 +330,27 @@ __device__ __forceinline__ void physics(Bodies& b, const float a[12]) {
     }
     b.bx = b.bx + b.bvx * K_H;
     b.by = b.by + b.bvy * K_H;
+    PROF_MARK(1)
+#ifndef VSS_PROF_SKIP_RR
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
       for (int j = i + 1; j < 6; ++j) contact_robot_robot(b, i, j);
+#endif
+    PROF_MARK(2)
+#ifndef VSS_PROF_SKIP_BR
 #pragma unroll
     for (int i = 0; i < 6; ++i) contact_ball_robot(b, i);
+#endif
+    PROF_MARK(3)
+#ifndef VSS_PROF_SKIP_WALLS
 #pragma unroll
     for (int i = 0; i < 6; ++i) contact_walls(b.x[i], b.y[i], b.vx[i], b.vy[i], K_ROBOT_R);
     contact_walls(b.bx, b.by, b.bvx, b.bvy, K_BALL_R);
+#endif
+    PROF_MARK(4)
   }
+  PROF_FLUSH
 }
 
 // ---- state I/O -----------------------------------------------------------------------------------
@@ -856,6 +889,16 @@ __global__ __launch_bounds__(kWave) void observe_kernel(int64_t n, vss_state s, 
 extern "C" {
 
 int vss_abi_version(void) { return VSS_ABI_VERSION; }
+
+#ifdef VSS_PROF_STAMPS
+// diagnostic builds only: copy (and clear) the 5 per-phase cycle sums
+int vss_prof_read(unsigned long long* host_out) {
+  unsigned long long zero[8] = {0};
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(vss::g_prof), sizeof(zero)) != hipSuccess) return VSS_E_LAUNCH;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(vss::g_prof), zero, sizeof(zero)) != hipSuccess) return VSS_E_LAUNCH;
+  return VSS_OK;
+}
+#endif
 
 const char* vss_error_string(int code) {
   switch (code) {

@@ -66,6 +66,15 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         print(f"{name:20s} {e0.elapsed_time(e1) / K * 1e3:8.1f} us/step")
+        if hasattr(L, "vss_prof_read"):
+            buf = (ctypes.c_ulonglong * 8)()
+            L.vss_prof_read(buf)  # includes the warm-up launches too
+            L.vss_prof_read(buf) if False else None
+            waves = (n + 63) // 64 * (K + 20)
+            names = ["drive", "integrate", "robot-robot", "ball-robot", "walls"]
+            tot = sum(buf[:5])
+            print("   stamps (s_memtime ticks per wave-step): " + ", ".join(
+                f"{nm} {buf[i] / waves:.0f} ({100 * buf[i] / max(tot, 1):.0f}%)" for i, nm in enumerate(names)))
 
 
 if __name__ == "__main__":

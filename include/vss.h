@@ -165,6 +165,46 @@ int vss_reset_dones(void* stream, int64_t n_fields, const vss_params* params,
 int vss_compute_observations(void* stream, int64_t n_fields, const vss_state* st,
                              float* obs, int32_t n_agents);
 
+/* ---------------------------------------------------------------------------------------------
+ * Fused rollout policy: the reference Agent's actor and critic MLPs
+ * (ppo_continuous_action_isaacgym.py:127-164, 52 -> 256 -> 512 -> 512 -> 256 -> n_out, tanh)
+ * on the fp32 matrix cores, activations kept in registers across the five layers.
+ * ------------------------------------------------------------------------------------------- */
+
+/* floats needed for one network's packed weights (n_out = 1 critic, 2 or 6 actor); -1 if bad */
+int64_t vss_mlp_packed_size(int32_t n_out);
+
+/*
+ * Repack one network (torch nn.Linear layout: weights[i] is (out, in) row-major, biases[i] (out))
+ * into the kernel's lane order.  Call once per parameter update.
+ */
+int vss_mlp_pack(void* stream, int32_t n_out, const float* const* weights, const float* const* biases,
+                 float* packed);
+
+/*
+ * Agent.get_action_and_value (ppo…:157-164) on `rows` observations (rows, 52):
+ * mean = actor(obs); action = action_in if given, else mean + exp(logstd) * N(0,1) (Philox on
+ * (seed, counter, row)); log-prob and entropy summed over the n_act dims (torch Normal
+ * formulas); value = critic(obs).  With actor_packed == NULL only the critic runs
+ * (Agent.get_value, ppo…:154-155).  Any output pointer may be NULL.
+ */
+int vss_policy_forward(void* stream, int64_t rows, int32_t n_act, const float* obs,
+                       const float* actor_packed, const float* logstd, const float* critic_packed,
+                       uint64_t seed, uint64_t counter, const float* action_in, float* action_out,
+                       float* logprob_out, float* entropy_out, float* value_out, float* mean_out);
+
+/*
+ * vss_policy_forward with an optional row mask for the critic-only form (actor_packed == NULL):
+ * only rows with row_mask[row] != 0 (e.g. the step's dones) are evaluated and written.  Used
+ * for the terminal-observation values of the fields that reset (ppo…:272): for every other field
+ * the terminal observation equals the next observation, whose value the next step computes.
+ */
+int vss_value_forward_masked(void* stream, int64_t rows, int32_t n_act, const float* obs,
+                             const float* actor_packed, const float* logstd, const float* critic_packed,
+                             uint64_t seed, uint64_t counter, const float* action_in, float* action_out,
+                             float* logprob_out, float* entropy_out, float* value_out, float* mean_out,
+                             const int64_t* row_mask);
+
 #ifdef __cplusplus
 }
 #endif

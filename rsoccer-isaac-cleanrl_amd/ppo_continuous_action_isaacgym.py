@@ -81,6 +81,9 @@ def parse_args(argv=None):
     p.add_argument("--save-path", type=str, default="runs")
     p.add_argument("--num-updates", type=int, default=None, help="override total_timesteps // batch")
     p.add_argument("--log", type=b, default=True, nargs="?", const=True)
+    p.add_argument("--fused-policy", type=b, default=True, nargs="?", const=True,
+                   help="rollout forward with the fused HIP MLP kernel (vss_policy_forward); "
+                        "terminal values only for the fields that reset")
     p.add_argument("--amp", type=str, default="none", choices=["none", "bf16"],
                    help="bf16 autocast for the MLP GEMMs (off = the reference's fp32 numerics)")
     args = p.parse_args(argv)
@@ -292,6 +295,10 @@ def train(args):
 
     agent = Agent(envs).to(device)
     flat = FlatGrads(agent)
+    fused = None
+    if args.fused_policy and device.type == "cuda" and args.amp == "none":
+        from vss_amd.policy import FusedPolicy
+        fused = FusedPolicy(agent, seed=seed * 7919 + 17)
     optimizer = optim.Adam(agent.parameters(), lr=args.learning_rate, eps=1e-5)
     gen = torch.Generator(device=device).manual_seed(seed)
 
@@ -306,6 +313,7 @@ def train(args):
     next_timeouts = torch.zeros((T, E), device=device)
     values = torch.zeros((T, E), device=device)
     next_values = torch.zeros((T, E), device=device)
+    term_values = torch.zeros((T, E), device=device)  # fused path: critic(terminal obs) of reset fields
 
     global_step = 0
     start_time = time.time()
@@ -318,22 +326,36 @@ def train(args):
         t_roll = time.time()
         ep_ret = torch.zeros((), device=device)
         ep_cnt = torch.zeros((), device=device)
+        if fused is not None:
+            fused.refresh()  # weights changed in the last update
         for step in range(T):
             global_step += E * world
             obs[step] = next_obs
             with torch.no_grad(), autocast(args, device):
-                action, logprob, _, value = agent.get_action_and_value(next_obs)
+                if fused is not None:
+                    action, logprob, _, value = fused.get_action_and_value(next_obs)
+                else:
+                    action, logprob, _, value = agent.get_action_and_value(next_obs)
                 values[step] = value.flatten()
             actions[step] = action.float()
             logprobs[step] = logprob.float()
             next_obs, rewards[step], next_done, info = envs.step(action)
             next_dones[step] = next_done
             next_timeouts[step] = info["time_outs"]
-            with torch.no_grad(), autocast(args, device):
-                next_values[step] = agent.get_value(info["terminal_observation"]).reshape(1, -1)
+            if fused is not None:
+                # critic(terminal obs) only where the field reset (ppo…:272): elsewhere the terminal
+                # observation IS next_obs, whose value the next step's forward computes
+                fused.get_value_masked(info["terminal_observation"], next_done, term_values[step].view(E, 1))
+            else:
+                with torch.no_grad(), autocast(args, device):
+                    next_values[step] = agent.get_value(info["terminal_observation"]).reshape(1, -1)
             d = next_done.float()
             ep_ret += (info["r"]["return"] * d).sum()
             ep_cnt += d.sum()
+        if fused is not None:
+            v_last = fused.get_value(next_obs).view(1, E)
+            nxt = torch.cat([values[1:], v_last], 0)
+            next_values = torch.where(next_dones.bool(), term_values, nxt)
         if device.type == "cuda":
             torch.cuda.synchronize()
         t_roll = time.time() - t_roll

@@ -24,7 +24,8 @@ STATE_CHANNELS = 58
 CH_BALL_X, CH_BALL_Y, CH_BALL_VX, CH_BALL_VY = 0, 1, 2, 3
 CH_RX, CH_RY, CH_RQX, CH_RQY, CH_RQZ, CH_RQW, CH_RVX, CH_RVY, CH_RW = 4, 10, 16, 22, 28, 34, 40, 46, 52
 EXPORTED = ("vss_abi_version", "vss_error_string", "vss_step", "vss_rollout", "vss_reset_dones",
-            "vss_compute_observations")
+            "vss_compute_observations", "vss_mlp_packed_size", "vss_mlp_pack", "vss_policy_forward",
+            "vss_value_forward_masked")
 
 
 class VssParams(ctypes.Structure):
@@ -84,6 +85,14 @@ def load() -> ctypes.CDLL:
     L.vss_reset_dones.restype = ctypes.c_int
     L.vss_compute_observations.argtypes = [P, i64, P, P, i32]
     L.vss_compute_observations.restype = ctypes.c_int
+    L.vss_mlp_packed_size.argtypes = [i32]
+    L.vss_mlp_packed_size.restype = i64
+    L.vss_mlp_pack.argtypes = [P, i32, P, P, P]
+    L.vss_mlp_pack.restype = ctypes.c_int
+    L.vss_policy_forward.argtypes = [P, i64, i32, P, P, P, P, ctypes.c_uint64, ctypes.c_uint64] + [P] * 6
+    L.vss_policy_forward.restype = ctypes.c_int
+    L.vss_value_forward_masked.argtypes = [P, i64, i32, P, P, P, P, ctypes.c_uint64, ctypes.c_uint64] + [P] * 7
+    L.vss_value_forward_masked.restype = ctypes.c_int
     if L.vss_abi_version() != ABI_VERSION:
         raise NativeError(f"libvss_amd ABI {L.vss_abi_version()} != expected {ABI_VERSION}")
     _lib = L

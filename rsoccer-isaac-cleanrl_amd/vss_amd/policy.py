@@ -1,0 +1,112 @@
+"""Fused rollout policy: the reference Agent's forward (ppo_continuous_action_isaacgym.py:154-164)
+as one HIP kernel on the fp32 matrix cores (csrc/vss_policy.hip, include/vss.h `vss_policy_forward`).
+
+    fused = FusedPolicy(agent)          # packs actor + critic weights (lane order) on the device
+    fused.refresh()                     # after every optimizer step (weights changed)
+    action, logprob, entropy, value = fused.get_action_and_value(obs)
+    value = fused.get_value(obs)
+
+Results equal the torch Agent's within fp32 summation-order rounding (tests/test_policy.py);
+actions are sampled from the same Normal(mean, exp(logstd)) with a Philox stream instead of
+torch's generator.  Inference only (no autograd): the PPO update keeps the torch modules.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native as N
+
+
+class FusedPolicy:
+    def __init__(self, agent, seed: int = 0):
+        self.agent = agent
+        self.device = next(agent.parameters()).device
+        N.require_device(self.device)
+        self.n_act = int(agent.actor_logstd.shape[-1])
+        if self.n_act not in (2, 6):
+            raise ValueError("fused policy supports 2 (SA/DMA) or 6 (CMA) actions")
+        lib = N.load()
+        self._actor = torch.empty(lib.vss_mlp_packed_size(self.n_act), device=self.device)
+        self._critic = torch.empty(lib.vss_mlp_packed_size(1), device=self.device)
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.counter = 0
+        self.refresh()
+
+    @staticmethod
+    def _linears(seq):
+        return [m for m in seq if isinstance(m, torch.nn.Linear)]
+
+    def _pack(self, seq, n_out, out):
+        lins = self._linears(seq)
+        if len(lins) != 5:
+            raise ValueError("expected the reference Agent's 5-layer MLPs")
+        ws = [l.weight.detach().contiguous() for l in lins]
+        bs = [l.bias.detach().contiguous() for l in lins]
+        self._keep = ws + bs
+        wa = (ctypes.c_void_p * 5)(*[w.data_ptr() for w in ws])
+        ba = (ctypes.c_void_p * 5)(*[b.data_ptr() for b in bs])
+        N.check(N.load().vss_mlp_pack(N.stream_of(self.device), n_out, wa, ba, out.data_ptr()), "vss_mlp_pack")
+
+    @torch.no_grad()
+    def refresh(self):
+        """Re-pack the current actor / critic weights (call after optimizer.step())."""
+        self._pack(self.agent.actor_mean, self.n_act, self._actor)
+        self._pack(self.agent.critic, 1, self._critic)
+
+    def _run(self, obs, actor: bool, action=None):
+        obs = obs.reshape(-1, 52)
+        if obs.dtype != torch.float32 or not obs.is_contiguous() or obs.device != self.device:
+            obs = obs.to(self.device, torch.float32).contiguous()
+        rows = obs.shape[0]
+        dev = self.device
+        value = torch.empty((rows, 1), device=dev)
+        outs = [None] * 4
+        if actor:
+            act_out = torch.empty((rows, self.n_act), device=dev) if action is None else None
+            logp = torch.empty(rows, device=dev)
+            ent = torch.empty(rows, device=dev)
+            mean = torch.empty((rows, self.n_act), device=dev)
+            if action is not None:
+                action = action.to(dev, torch.float32).contiguous()
+            outs = [act_out, logp, ent, mean]
+        self.counter += 1
+        rc = N.load().vss_policy_forward(
+            N.stream_of(dev), rows, self.n_act, obs.data_ptr(), self._actor.data_ptr() if actor else None,
+            self.agent.actor_logstd.detach().data_ptr(), self._critic.data_ptr(), self.seed, self.counter,
+            N.ptr(action), N.ptr(outs[0]), N.ptr(outs[1]), N.ptr(outs[2]), value.data_ptr(), N.ptr(outs[3]))
+        N.check(rc, "vss_policy_forward")
+        if actor:
+            return (action if action is not None else outs[0]), outs[1], outs[2], value, outs[3]
+        return value
+
+    @torch.no_grad()
+    def get_action_and_value(self, obs, action=None):
+        a, logp, ent, value, _ = self._run(obs, True, action)
+        return a, logp, ent, value
+
+    @torch.no_grad()
+    def get_value(self, obs):
+        return self._run(obs, False)
+
+    @torch.no_grad()
+    def get_value_masked(self, obs, mask: torch.Tensor, out: torch.Tensor):
+        """critic(obs) written into `out` (rows, 1) only for rows with mask != 0 (int64 mask,
+        e.g. the env's dones); other rows of `out` are left untouched."""
+        obs = obs.reshape(-1, 52)
+        rows = obs.shape[0]
+        if mask.dtype != torch.long:
+            mask = mask.long()
+        mask = mask.contiguous()
+        if out.numel() != rows or not out.is_contiguous() or mask.numel() != rows:
+            raise ValueError("out / mask must have one element per row")
+        rc = N.load().vss_value_forward_masked(
+            N.stream_of(self.device), rows, self.n_act, obs.contiguous().data_ptr(), None, None,
+            self._critic.data_ptr(), self.seed, 0, None, None, None, None, out.data_ptr(), None, mask.data_ptr())
+        N.check(rc, "vss_value_forward_masked")
+        return out
+
+    @torch.no_grad()
+    def actor_mean(self, obs):
+        return self._run(obs, True)[4]

@@ -12,7 +12,7 @@ from vss_amd import _native as N
 def declared_functions():
     src = open(N.HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(vss_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int64_t|int|const char\*)\s+(vss_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_header_declares_the_expected_entry_points():

@@ -174,3 +174,39 @@ def test_train_end_to_end_gpu(env_id, tmp_path):
             assert np.isfinite(h[k]), (k, h)
         assert h["sps"] > 0
     assert os.path.exists(os.path.join(tmp_path, f"{args.exp_name}_ppo-{env_id}_1", f"{args.exp_name}_ppo-{env_id}_1-agent.pt"))
+
+
+@pytest.mark.gpu
+def test_fused_rollout_next_values_equal_reference_definition(tmp_path):
+    """With the fused policy the PPO loop reconstructs next_values[t] = critic(terminal_obs_t)
+    (ppo…:272) from values[t+1] and the masked terminal pass.  Check the identity directly: run a
+    short SA rollout and compare with critic(terminal_obs) evaluated for every row."""
+    from envs.vss import default_cfg
+    from envs.wrappers import SingleAgent
+    from envs.vss import VSS
+    from vss_amd.policy import FusedPolicy
+    cfg = default_cfg(2048)
+    cfg["env"]["maxEpisodeLength"] = 8
+    cfg["env"]["seed"] = 5
+    env = VSS(cfg, "cuda:0", "cuda:0", 0, True, False, False)
+    W = SingleAgent(env)
+    agent = make_agent(2).cuda()
+    fused = FusedPolicy(agent, seed=1)
+    T, E = 12, 2048
+    values = torch.zeros((T, E), device="cuda")
+    term = torch.zeros((T, E), device="cuda")
+    full = torch.zeros((T, E), device="cuda")
+    dones = torch.zeros((T, E), device="cuda")
+    o = W.reset()["obs"]
+    for t in range(T):
+        a, lp, _, v = fused.get_action_and_value(o)
+        values[t] = v.flatten()
+        ob, r, d, info = W.step(a)
+        dones[t] = d
+        fused.get_value_masked(info["terminal_observation"], d, term[t].view(E, 1))
+        full[t] = fused.get_value(info["terminal_observation"]).flatten()
+        o = ob["obs"]
+    v_last = fused.get_value(o).view(1, E)
+    nv = torch.where(dones.bool(), term, torch.cat([values[1:], v_last], 0))
+    assert dones.sum() > 0
+    assert torch.equal(nv, full)

@@ -52,4 +52,22 @@ case ",$STEPS," in *,sq,*)
   run rocprof_sq2 400 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM_WR SQ_INSTS_SMEM GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_sq2_$TAG" -o run -- \
       python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
 esac
+case ",$STEPS," in *,profall,*)
+  run prof_full 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \
+      python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline --ppo-updates 0 --rollout-k 16
+  run prof_sa 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_sa_$TAG" -o run -- \
+      python3 bench.py --mode sa --steps 100 --warmup 10 --no-cpu-baseline --ppo-updates 0
+  run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$TAG" -o run -- \
+      python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --ppo-updates 0 --rollout-k 0
+  run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$TAG" -o run -- \
+      python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --ppo-updates 0 --rollout-k 0
+  run pmc_fetch_sa 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_sa_$TAG" -o run -- \
+      python3 bench.py --mode sa --steps 20 --warmup 5 --no-cpu-baseline --ppo-updates 0
+  run pmc_write_sa 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_sa_$TAG" -o run -- \
+      python3 bench.py --mode sa --steps 20 --warmup 5 --no-cpu-baseline --ppo-updates 0
+  run prof_policy 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_policy_$TAG" -o run -- \
+      python3 tools/policy_bench.py
+  run pmc_policy 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_WAVES SQ_BUSY_CYCLES --output-format csv -d "$OUT/pmc_policy_$TAG" -o run -- \
+      python3 tools/policy_bench.py ;;
+esac
 echo "session done" | tee -a "$OUT/session.log"

@@ -37,21 +37,25 @@ def main():
     ap.add_argument("--fields", type=int, default=65536)
     ap.add_argument("--mode", default="full")
     ap.add_argument("--algo-bytes", type=int, default=3101)
+    ap.add_argument("--suffix", default="", help="pmc dir suffix, e.g. '_sa' for pmc_fetch_sa_<tag>")
+    ap.add_argument("--stats-dir", default=None, help="kernel-trace dir name (default prof_<tag>)")
+    ap.add_argument("--out", default="pmc_traffic.json")
     args = ap.parse_args()
     out_dir = os.path.join(REPO, "profiles")
     os.makedirs(out_dir, exist_ok=True)
     g = os.path.join(REPO, "gpurun_out")
     res = {"tag": args.tag, "kernel": args.kernel, "fields": args.fields, "mode": args.mode}
 
-    stats = os.path.join(g, f"prof_{args.tag}", "run_kernel_stats.csv")
+    sdir = args.stats_dir or f"prof_{args.tag}"
+    stats = os.path.join(g, sdir, "run_kernel_stats.csv")
     if os.path.exists(stats):
-        shutil.copy(stats, os.path.join(out_dir, f"{args.tag}_kernel_stats.csv"))
+        shutil.copy(stats, os.path.join(out_dir, f"{args.tag}_{sdir.replace('_' + args.tag, '')}_kernel_stats.csv"))
         for r in csv.DictReader(open(stats)):
             if args.kernel in r["Name"]:
                 res["avg_ns"] = float(r["AverageNs"])
                 res["calls"] = int(r["Calls"])
-    fpath = os.path.join(g, f"pmc_fetch_{args.tag}", "run_counter_collection.csv")
-    wpath = os.path.join(g, f"pmc_write_{args.tag}", "run_counter_collection.csv")
+    fpath = os.path.join(g, f"pmc_fetch{args.suffix}_{args.tag}", "run_counter_collection.csv")
+    wpath = os.path.join(g, f"pmc_write{args.suffix}_{args.tag}", "run_counter_collection.csv")
     if os.path.exists(fpath) and os.path.exists(wpath):
         fetch = counters(fpath, args.kernel)["FETCH_SIZE"]
         write = counters(wpath, args.kernel)["WRITE_SIZE"]
@@ -68,7 +72,7 @@ def main():
                 w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
                 w.writeheader()
                 w.writerows(rows)
-        with open(os.path.join(out_dir, "pmc_traffic.json"), "w") as f:
+        with open(os.path.join(out_dir, args.out), "w") as f:
             json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
 

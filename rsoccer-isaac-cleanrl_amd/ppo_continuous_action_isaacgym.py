@@ -18,6 +18,7 @@ clipped-PPO update semantics (ppo…:231-365).  MI355X-first changes:
 from __future__ import annotations
 
 import argparse
+import json
 import os
 import random
 import sys
@@ -386,6 +387,10 @@ def train(args):
     if rank == 0 and args.log:
         os.makedirs(f"{args.save_path}/{run_name}", exist_ok=True)
         torch.save(agent.state_dict(), f"{args.save_path}/{run_name}/{run_name}-agent.pt")
+        # the loss / SPS curves (what the reference sends to TensorBoard/W&B), one record per update
+        with open(f"{args.save_path}/{run_name}/history.json", "w") as f:
+            json.dump({"args": vars(args), "world": world, "wall_s": time.time() - start_time,
+                       "history": history}, f, indent=1)
     writer.close()
     return agent, history
 

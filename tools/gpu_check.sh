@@ -46,6 +46,14 @@ case ",$STEPS," in *,ppoprof,*)
       python3 rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 1 --log false ;;
 esac
 case ",$STEPS," in *,ppo,*) run ppo_sa 900 python rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 2 --save-path /tmp/runs ;; esac
+# the full SA run to >= 1e8 env-steps (12 updates of 65,536 x 128), with its
+# loss curves; config 4: DMA at 65,536 fields (196,608 agent rows), a short run + the step bench
+case ",$STEPS," in *,ppo1e8,*)
+  run ppo_sa_1e8 900 python rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 \
+      --total-timesteps 100663296 --save-path "$OUT/runs_$TAG" && \
+  run ppo_dma 900 python rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id dma --num-envs 196608 \
+      --num-updates 2 --save-path "$OUT/runs_$TAG" && \
+  run bench_dma 300 python bench.py --mode dma --no-cpu-baseline --ppo-updates 0 ;; esac
 case ",$STEPS," in *,sq,*)
   run rocprof_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY --output-format csv -d "$OUT/pmc_sq_$TAG" -o run -- \
       python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline

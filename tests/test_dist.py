@@ -43,14 +43,17 @@ def test_bench_timing_is_max_over_ranks_gloo():
 
 
 @pytest.mark.gpu
-def test_bench_two_ranks_rehearsal():
-    """bench.py as the driver launches it for N>1 (torch.distributed.run), 2 ranks sharing the
-    one GPU with gloo for the barrier/timing reduce: one JSON line, value counts both ranks."""
+@pytest.mark.parametrize("launcher", ["torchrun", "self"])
+def test_bench_two_ranks_rehearsal(launcher):
+    """bench.py as the driver launches it for N>1 (torch.distributed.run) and as a user runs it
+    by hand (`bench.py --gpus 2` starts the launcher itself), 2 ranks sharing the one GPU with
+    gloo for the barrier/timing reduce: one JSON line, value counts both ranks."""
     port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--steps", "20", "--warmup", "2", "--fields", "8192", "--dist-backend", "gloo",
-           "--share-gpu", "--no-cpu-baseline"]
+    run = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port)] if launcher == "torchrun" else [sys.executable]
+    cmd = run + [os.path.join(REPO, "bench.py"),
+                 "--gpus", "2", "--steps", "20", "--warmup", "2", "--fields", "8192", "--dist-backend", "gloo",
+                 "--share-gpu", "--no-cpu-baseline"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]

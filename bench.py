@@ -307,7 +307,9 @@ def main():
         algo = BYTES[args.mode] * n
         achieved = algo / (kern_ms * 1e-3)
         traffic = None
-        tfile = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        # HBM bytes per launch from the committed rocprofv3 PMC passes of the same command
+        # (tools/pmc_summary.py; null when no profile matches this mode and size)
+        tfile = os.path.join(REPO, "profiles", "pmc_traffic.json" if args.mode == "full" else f"pmc_traffic_{args.mode}.json")
         if os.path.exists(tfile):
             try:
                 tj = json.load(open(tfile))

@@ -24,6 +24,34 @@
 namespace vss {
 
 constexpr int kWave = 64;
+// Fields per step/rollout wave (one wave per workgroup; all 64 lanes take part in the streams),
+// per contract.  FULL and DMA: 32, not 64 — at 65,536 fields that is 2,048 waves = 2 per SIMD, so
+// one wave's physics (a latency-bound dependency chain, ~1 VALU issue per 4+ cycles) overlaps the
+// other wave's observation stores.  Measured (tools/ablate.py): FULL step 48.8 -> 42.7 us, rollout
+// 39.7 -> 33.8 us/step; 16 and 24 are slower (156 VGPRs allow 3 waves per SIMD: the grid no longer
+// fits in one round).  SA / CMA move a third of the bytes, so there is little store stream to
+// hide the physics behind and half-empty waves cost more issue slots than they save: 64.
+#ifndef VSS_FPW_FULL
+#define VSS_FPW_FULL 32
+#endif
+#ifndef VSS_FPW_SA
+#define VSS_FPW_SA 64
+#endif
+#ifndef VSS_FPW_CMA
+#define VSS_FPW_CMA 64
+#endif
+#ifndef VSS_FPW_DMA
+#define VSS_FPW_DMA 32
+#endif
+template <int MODE>
+constexpr int fields_per_wave() {
+  return MODE == VSS_MODE_FULL ? VSS_FPW_FULL
+         : MODE == VSS_MODE_SA ? VSS_FPW_SA
+         : MODE == VSS_MODE_CMA ? VSS_FPW_CMA : VSS_FPW_DMA;
+}
+constexpr int kFpwRollout = VSS_FPW_FULL;  // the rollout kernel runs the FULL contract
+static_assert(fields_per_wave<0>() <= kWave && fields_per_wave<1>() <= kWave && fields_per_wave<2>() <= kWave &&
+              fields_per_wave<3>() <= kWave, "fields per wave");
 constexpr int kRec = 59;  // LDS floats per field record (58 used, odd stride: no bank conflicts)
 
 // ---- model constants (reference values cited in oracle/vss_oracle.c) --------
@@ -550,12 +578,16 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
 
   const int64_t n = args.n;
   const int lane = threadIdx.x;
-  const int64_t f0 = (int64_t)blockIdx.x * kWave;
-  const int nv = (int)(n - f0 < kWave ? n - f0 : kWave);
+  constexpr int kFpw = fields_per_wave<MODE>();
+  const int64_t f0 = (int64_t)blockIdx.x * kFpw;
+  const int nv = (int)(n - f0 < kFpw ? n - f0 : kFpw);
   const int64_t f = f0 + lane;
   const bool valid = lane < nv;
   const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
   float* rec = lds + lane * kRec;
+#if defined(VSS_PROF_PRIO)  // profiling-only experiment: raise half of the waves' issue priority
+  if (VSS_PROF_PRIO == 1 ? blockIdx.x < gridDim.x / 2 : (blockIdx.x & 1) != 0) __builtin_amdgcn_s_setprio(3);
+#endif
 
   // -- state loads first (46 coalesced channel loads in flight), then the action transpose -------
   int64_t progress = 0, reset_prev = 0;
@@ -762,8 +794,8 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
   __shared__ float lds[kWave * kRec];
   const int64_t n = args.n;
   const int lane = threadIdx.x;
-  const int64_t f0 = (int64_t)blockIdx.x * kWave;
-  const int nv = (int)(n - f0 < kWave ? n - f0 : kWave);
+  const int64_t f0 = (int64_t)blockIdx.x * kFpwRollout;
+  const int nv = (int)(n - f0 < kFpwRollout ? n - f0 : kFpwRollout);
   const int64_t f = f0 + lane;
   const bool valid = lane < nv;
   const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
@@ -928,7 +960,10 @@ int vss_step(void* stream, int64_t n, int32_t mode, const vss_params* p, const v
   if (mode == VSS_MODE_DMA && !io->dones_rep) return VSS_E_ARG;
   if (n == 0) return VSS_OK;
   vss::StepArgs args{n, *p, *st, *io};
-  const dim3 grid((unsigned)((n + vss::kWave - 1) / vss::kWave)), block(vss::kWave);
+  const int fpw = mode == VSS_MODE_FULL ? vss::fields_per_wave<VSS_MODE_FULL>()
+                  : mode == VSS_MODE_SA ? vss::fields_per_wave<VSS_MODE_SA>()
+                  : mode == VSS_MODE_CMA ? vss::fields_per_wave<VSS_MODE_CMA>() : vss::fields_per_wave<VSS_MODE_DMA>();
+  const dim3 grid((unsigned)((n + fpw - 1) / fpw)), block(vss::kWave);
   hipStream_t s = (hipStream_t)stream;
   switch (mode) {
     case VSS_MODE_FULL: hipLaunchKernelGGL(vss::step_kernel<VSS_MODE_FULL>, grid, block, 0, s, args); break;
@@ -947,7 +982,7 @@ int vss_rollout(void* stream, int64_t n, int32_t k_steps, const vss_params* p, c
     return VSS_E_ARG;
   if (n == 0) return VSS_OK;
   vss::RolloutArgs args{n, k_steps, *p, *st, *io};
-  const dim3 grid((unsigned)((n + vss::kWave - 1) / vss::kWave)), block(vss::kWave);
+  const dim3 grid((unsigned)((n + vss::kFpwRollout - 1) / vss::kFpwRollout)), block(vss::kWave);
   hipLaunchKernelGGL(vss::rollout_kernel, grid, block, 0, (hipStream_t)stream, args);
   return launch_status();
 }

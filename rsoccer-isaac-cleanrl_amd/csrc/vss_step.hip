@@ -88,8 +88,21 @@ constexpr uint32_t kPurposeOU = 1u, kPurposePos = 2u, kPurposeAng = 3u, kExterna
 // ---- observation gather table ---------------------------------------------------------------
 // For float4 index j4 (0..77) of a field's (6, 52) observation block: 4 bytes, each
 // (source index into the 58-float LDS record) | 0x80 if the value is negated (yellow mirror).
+// Observation records in LDS.  Plain record (kRec = 59 floats): ball (4) + 6 x (x, y, vx, vy, cos,
+// sin, w, aL, aR).  The FULL contract (A = 6 agents) appends the 40 slots that the yellow view
+// negates (ball 4 + 6 x (x, y, vx, vy, cos, sin)), already negated: the streams then gather plain
+// copies only.  Record stride kRecObs6 = 99 floats (odd: conflict-free per-lane writes).
+constexpr int kRecObs6 = kRec + 40;
+template <int A>
+constexpr int obs_rec() { return A == 6 ? kRecObs6 : kRec; }
+constexpr int mirror_slot(int src) { return src < 4 ? kRec + src : kRec + 4 + ((src - 4) / 9) * 6 + (src - 4) % 9; }
+
+// Gather table for the (2,3,52) per-field observation block, one entry per float4: two words,
+// each two 16-bit LDS byte offsets within the field's record (source slot x 4; yellow-view
+// negated values point into the mirror slots).  A < 6 contracts use the first 13 x A entries
+// (blue agents: no mirror slots), so one table serves every record stride.
 struct ObsTable {
-  uint32_t w[78];
+  uint32_t w[2 * 78];
 };
 
 constexpr ObsTable make_obs_table() {
@@ -112,8 +125,8 @@ constexpr ObsTable make_obs_table() {
       src = 4 + r * 9 + q;
       neg = team == 1 && q < 6;
     }
-    uint32_t byte = (uint32_t)src | (neg ? 0x80u : 0u);
-    t.w[j / 4] |= byte << (8 * (j % 4));
+    uint32_t off = 4u * (uint32_t)(neg ? mirror_slot(src) : src);
+    t.w[j / 2] |= off << (16 * (j % 2));
   }
   return t;
 }
@@ -450,7 +463,8 @@ __device__ __forceinline__ void coop_store(float* __restrict__ g, int nv, const 
   }
 }
 
-// Observation record of one field into LDS: ball (4) + 6 x (x, y, vx, vy, cos, sin, w, aL, aR).
+// Observation record of one field into LDS (layout above); A = 6 also writes the mirror slots.
+template <int A>
 __device__ __forceinline__ void write_obs_record(float* rec, const Bodies& b, const float dof[12]) {
   rec[0] = b.bx; rec[1] = b.by; rec[2] = b.bvx; rec[3] = b.bvy;
 #pragma unroll
@@ -461,24 +475,53 @@ __device__ __forceinline__ void write_obs_record(float* rec, const Bodies& b, co
     o[5] = 2.0f * b.qw[r] * b.qz[r];
     o[6] = b.w[r]; o[7] = dof[2 * r]; o[8] = dof[2 * r + 1];
   }
+  if constexpr (A == 6) {
+    // negation = sign-bit flip (what mirror_tensor's multiply by -1 gives, incl. -0 for 0)
+    float* m = rec + kRec;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) m[k] = __uint_as_float(__float_as_uint(rec[k]) ^ 0x80000000u);
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+        m[4 + 6 * r + q] = __uint_as_float(__float_as_uint(rec[4 + 9 * r + q]) ^ 0x80000000u);
+  }
 }
 
-// Stream the wave's observation block (nv fields x A agents x 52) out of the LDS records.
+// Stream the wave's observation block (nv fields x A agents x 52) out of the LDS records: each
+// lane walks float4 slots q = lane, lane + 64, ... with its (field, slot) position advanced
+// incrementally; four LDS reads per float4 at table-given byte offsets, one 16-B store.  Unrolled
+// by kObsUnroll so the LDS latency of U slots overlaps (reads past the last field are clamped to
+// the last record and their stores predicated off).
+constexpr int kObsUnroll = 4;
 template <int A>
 __device__ __forceinline__ void coop_store_obs(float* __restrict__ out, int nv, const float* lds, int lane) {
   constexpr int Q = 13 * A;  // float4 per field
+  constexpr int QD = kWave / Q, QR = kWave % Q;
+  constexpr uint32_t RB = 4u * obs_rec<A>();  // record bytes
   const int total = nv * Q;
+  const uint32_t rb_last = (uint32_t)(nv - 1) * RB;
+  int fl = lane / Q, j4 = lane - fl * Q;
+  uint32_t rb = (uint32_t)fl * RB;
+  const char* L = reinterpret_cast<const char*>(lds);
   float4* o4 = reinterpret_cast<float4*>(out);
-  for (int q = lane; q < total; q += kWave) {
-    int fl = q / Q, j4 = q - fl * Q;
-    uint32_t t = kObsTab.w[j4];
-    const float* rec = lds + fl * kRec;
-    float4 v;
-    v.x = __uint_as_float(__float_as_uint(rec[t & 0x7fu]) ^ ((t & 0x80u) << 24));
-    v.y = __uint_as_float(__float_as_uint(rec[(t >> 8) & 0x7fu]) ^ ((t & 0x8000u) << 16));
-    v.z = __uint_as_float(__float_as_uint(rec[(t >> 16) & 0x7fu]) ^ ((t & 0x800000u) << 8));
-    v.w = __uint_as_float(__float_as_uint(rec[(t >> 24) & 0x7fu]) ^ (t & 0x80000000u));
-    o4[q] = v;
+  for (int q0 = lane; q0 < total; q0 += kObsUnroll * kWave) {
+    float4 v[kObsUnroll];
+#pragma unroll
+    for (int u = 0; u < kObsUnroll; ++u) {
+      const uint2 t = reinterpret_cast<const uint2*>(kObsTab.w)[j4];  // constant table (L1/K$-resident)
+      const uint32_t r = rb < rb_last ? rb : rb_last;
+      v[u].x = *reinterpret_cast<const float*>(L + r + (t.x & 0xffffu));
+      v[u].y = *reinterpret_cast<const float*>(L + r + (t.x >> 16));
+      v[u].z = *reinterpret_cast<const float*>(L + r + (t.y & 0xffffu));
+      v[u].w = *reinterpret_cast<const float*>(L + r + (t.y >> 16));
+      j4 += QR;
+      rb += QD * RB;
+      if (j4 >= Q) { j4 -= Q; rb += RB; }
+    }
+#pragma unroll
+    for (int u = 0; u < kObsUnroll; ++u)
+      if (q0 + u * kWave < total) o4[q0 + u * kWave] = v[u];
   }
 }
 
@@ -574,17 +617,19 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   constexpr int A = MODE == VSS_MODE_FULL ? 6 : (MODE == VSS_MODE_DMA ? 3 : 1);
   constexpr int R = MODE == VSS_MODE_DMA ? 3 : 1;
   constexpr int NL = MODE == VSS_MODE_SA ? 2 : 6;  // learner action floats per field
+  constexpr int kFpw = fields_per_wave<MODE>();
+  static_assert(kFpw * obs_rec<A>() <= kWave * kRec, "observation records must fit the LDS block");
   __shared__ float lds[kWave * kRec];
 
   const int64_t n = args.n;
   const int lane = threadIdx.x;
-  constexpr int kFpw = fields_per_wave<MODE>();
   const int64_t f0 = (int64_t)blockIdx.x * kFpw;
   const int nv = (int)(n - f0 < kFpw ? n - f0 : kFpw);
   const int64_t f = f0 + lane;
   const bool valid = lane < nv;
   const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
   float* rec = lds + lane * kRec;
+  float* orec = lds + lane * obs_rec<A>();  // observation record (lanes < kFpw)
 #if defined(VSS_PROF_PRIO)  // profiling-only experiment: raise half of the waves' issue priority
   if (VSS_PROF_PRIO == 1 ? blockIdx.x < gridDim.x / 2 : (blockIdx.x & 1) != 0) __builtin_amdgcn_s_setprio(3);
 #endif
@@ -666,7 +711,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   const int64_t done = rewards_and_done(args.p, b, pbx, pby, prx, pry, a, progress, rew);
 
   // -- terminal observation (envs/vss.py:195-196) ----------------------------------------------------------
-  write_obs_record(rec, b, a);
+  if (lane < kFpw) write_obs_record<A>(orec, b, a);
   __syncthreads();
 #ifndef VSS_PROF_SKIP_OBS
   coop_store_obs<A>(args.io.terminal_obs + f0 * (52 * A), nv, lds, lane);
@@ -684,7 +729,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   }
 
   // -- observation after reset (envs/vss.py:203) -------------------------------------------------------------
-  write_obs_record(rec, b, dof);
+  if (lane < kFpw) write_obs_record<A>(orec, b, dof);
   __syncthreads();
 #ifndef VSS_PROF_SKIP_OBS
   coop_store_obs<A>(args.io.obs + f0 * (52 * A), nv, lds, lane);
@@ -791,6 +836,7 @@ __device__ __forceinline__ void stage12(const float4 pre[3], int nv, float* lds,
 }
 
 __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
+  static_assert(kFpwRollout * kRecObs6 <= kWave * kRec, "observation records must fit the LDS block");
   __shared__ float lds[kWave * kRec];
   const int64_t n = args.n;
   const int lane = threadIdx.x;
@@ -800,6 +846,7 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
   const bool valid = lane < nv;
   const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
   float* rec = lds + lane * kRec;
+  float* orec = lds + lane * kRecObs6;  // observation record (lanes < kFpwRollout)
 
   int64_t progress = 0, reset_prev = 0;
   uint32_t ctr = 0;
@@ -835,7 +882,7 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
     float rew[24];
     done = rewards_and_done(args.p, b, pbx, pby, prx, pry, a, progress, rew);
 
-    write_obs_record(rec, b, a);
+    if (lane < kFpwRollout) write_obs_record<6>(orec, b, a);
     __syncthreads();
     coop_store_obs<6>(args.io.terminal_obs + (step_off + f0) * 312, nv, lds, lane);
     __syncthreads();
@@ -846,7 +893,7 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
 #pragma unroll
       for (int i = 0; i < 12; ++i) dof[i] = dof[i] * 0.0f;
     }
-    write_obs_record(rec, b, dof);
+    if (lane < kFpwRollout) write_obs_record<6>(orec, b, dof);
     __syncthreads();
     coop_store_obs<6>(args.io.obs + (step_off + f0) * 312, nv, lds, lane);
     __syncthreads();
@@ -892,12 +939,13 @@ __global__ __launch_bounds__(kWave) void reset_kernel(int64_t n, vss_params p, v
 
 template <int A>
 __global__ __launch_bounds__(kWave) void observe_kernel(int64_t n, vss_state s, float* obs) {
-  __shared__ float lds[kWave * kRec];
+  __shared__ float lds[kWave * obs_rec<A>()];
   const int lane = threadIdx.x;
   const int64_t f0 = (int64_t)blockIdx.x * kWave;
   const int nv = (int)(n - f0 < kWave ? n - f0 : kWave);
   const int64_t f = f0 + lane;
   float* rec = lds + lane * kRec;
+  float* orec = lds + lane * obs_rec<A>();
   coop_load<12>(s.dof_velocity_buf + f0 * 12, nv, lds, lane);
   __syncthreads();
   float dof[12];
@@ -907,7 +955,7 @@ __global__ __launch_bounds__(kWave) void observe_kernel(int64_t n, vss_state s, 
   Bodies b = {};
   if (lane < nv) {
     load_bodies(s.state, n, f, b);
-    write_obs_record(rec, b, dof);
+    write_obs_record<A>(orec, b, dof);
   }
   __syncthreads();
   coop_store_obs<A>(obs + f0 * (52 * A), nv, lds, lane);

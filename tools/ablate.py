@@ -62,6 +62,8 @@ def main():
     stream = N.stream_of(env.device)
     import glob
     names = sorted(os.path.basename(p)[7:-3] for p in glob.glob(os.path.join(REPO, "tools", "_build", "libvss_*.so")))
+    if os.environ.get("ABLATE_ONLY"):  # one variant per process (rocprofv3 --pmc passes)
+        names = [nm for nm in names if nm == os.environ["ABLATE_ONLY"]]
     libs = []
     for name in names:
         L = ctypes.CDLL(os.path.join(REPO, "tools", "_build", f"libvss_{name}.so"))

@@ -25,20 +25,20 @@ namespace vss {
 
 constexpr int kWave = 64;
 // Fields per step/rollout wave (one wave per workgroup; all 64 lanes take part in the streams),
-// per contract.  FULL and DMA: 32, not 64 — at 65,536 fields that is 2,048 waves = 2 per SIMD, so
-// one wave's physics (a latency-bound dependency chain, ~1 VALU issue per 4+ cycles) overlaps the
-// other wave's observation stores.  Measured (tools/ablate.py): FULL step 48.8 -> 42.7 us, rollout
-// 39.7 -> 33.8 us/step; 16 and 24 are slower (156 VGPRs allow 3 waves per SIMD: the grid no longer
-// fits in one round).  SA / CMA move a third of the bytes, so there is little store stream to
-// hide the physics behind and half-empty waves cost more issue slots than they save: 64.
+// per contract.  32, not 64: at 65,536 fields that is 2,048 waves = 2 per SIMD, so one wave's
+// physics overlaps the other wave's stores, and lanes L and L + 32 share a field, splitting its
+// per-robot physics (physics_split).  Measured (tools/ablate.py, profiles/r01_ablate_*):
+// FULL 48.8 -> 42.7 us with 32 fields per wave, -> 40.8 us with the split; SA 27.2 -> 25.9 us.
+// 16 and 24 are slower (LDS and VGPRs allow fewer than 3 waves per SIMD: the grid no longer fits
+// in one round).
 #ifndef VSS_FPW_FULL
 #define VSS_FPW_FULL 32
 #endif
 #ifndef VSS_FPW_SA
-#define VSS_FPW_SA 64
+#define VSS_FPW_SA 32
 #endif
 #ifndef VSS_FPW_CMA
-#define VSS_FPW_CMA 64
+#define VSS_FPW_CMA 32
 #endif
 #ifndef VSS_FPW_DMA
 #define VSS_FPW_DMA 32
@@ -327,6 +327,38 @@ __device__ __forceinline__ void contact_walls(float& x, float& y, float& vx, flo
   x = ax * sx; y = ay * sy; vx = avx * sx; vy = avy * sy;
 }
 
+// One robot's traction-limited differential drive (spec §3) and its explicit integration step
+// (position, yaw quaternion with one Newton renormalisation, heading).  Shared by both physics
+// forms below, so every robot sees the identical operation sequence.
+__device__ __forceinline__ void drive_robot(float c, float s, float& vx, float& vy, float& w, float tl, float tr) {
+  float vf = c * vx + s * vy;
+  float vl = c * vy - s * vx;
+  float wl = vf - w * K_HALF_TRACK;
+  float wr = vf + w * K_HALF_TRACK;
+  wl = wl + clampf(tl - wl, -K_DV, K_DV);
+  wr = wr + clampf(tr - wr, -K_DV, K_DV);
+  vf = (wl + wr) * 0.5f;
+  w = (wr - wl) * K_INV_TRACK;
+  vl = vl - clampf(vl, -K_DL, K_DL);
+  vx = c * vf - s * vl;
+  vy = s * vf + c * vl;
+}
+
+__device__ __forceinline__ void integrate_robot(float& x, float& y, float vx, float vy, float w, float& qz, float& qw,
+                                                float& c, float& s) {
+  x = x + vx * K_H;
+  y = y + vy * K_H;
+  float sh, ch;
+  sincos_small(w * K_HH, sh, ch);
+  const float nqz = qz * ch + qw * sh;
+  const float nqw = qw * ch - qz * sh;
+  const float k = 1.5f - 0.5f * (nqz * nqz + nqw * nqw);  // one Newton step of 1/|q|
+  qz = nqz * k;
+  qw = nqw * k;
+  c = qw * qw - qz * qz;
+  s = 2.0f * qw * qz;
+}
+
 __device__ __forceinline__ void physics(Bodies& b, const float a[12]) {
   PROF_DECL
   float tl[6], tr[6];
@@ -339,36 +371,13 @@ __device__ __forceinline__ void physics(Bodies& b, const float a[12]) {
 #pragma unroll 1
   for (int sub = 0; sub < NSUB; ++sub) {
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      float c = b.c[i], s = b.s[i];
-      float vf = c * b.vx[i] + s * b.vy[i];
-      float vl = c * b.vy[i] - s * b.vx[i];
-      float wl = vf - b.w[i] * K_HALF_TRACK;
-      float wr = vf + b.w[i] * K_HALF_TRACK;
-      wl = wl + clampf(tl[i] - wl, -K_DV, K_DV);
-      wr = wr + clampf(tr[i] - wr, -K_DV, K_DV);
-      vf = (wl + wr) * 0.5f;
-      b.w[i] = (wr - wl) * K_INV_TRACK;
-      vl = vl - clampf(vl, -K_DL, K_DL);
-      b.vx[i] = c * vf - s * vl;
-      b.vy[i] = s * vf + c * vl;
-    }
+    for (int i = 0; i < 6; ++i) drive_robot(b.c[i], b.s[i], b.vx[i], b.vy[i], b.w[i], tl[i], tr[i]);
     PROF_MARK(0)
     b.bvx = b.bvx * K_BALL_DAMP;
     b.bvy = b.bvy * K_BALL_DAMP;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      b.x[i] = b.x[i] + b.vx[i] * K_H;
-      b.y[i] = b.y[i] + b.vy[i] * K_H;
-      float sh, ch;
-      sincos_small(b.w[i] * K_HH, sh, ch);
-      float qz = b.qz[i] * ch + b.qw[i] * sh;
-      float qw = b.qw[i] * ch - b.qz[i] * sh;
-      float k = 1.5f - 0.5f * (qz * qz + qw * qw);  // one Newton step of 1/|q|
-      b.qz[i] = qz * k;
-      b.qw[i] = qw * k;
-      heading(b, i);
-    }
+    for (int i = 0; i < 6; ++i)
+      integrate_robot(b.x[i], b.y[i], b.vx[i], b.vy[i], b.w[i], b.qz[i], b.qw[i], b.c[i], b.s[i]);
     b.bx = b.bx + b.bvx * K_H;
     b.by = b.by + b.bvy * K_H;
     PROF_MARK(1)
@@ -392,6 +401,96 @@ __device__ __forceinline__ void physics(Bodies& b, const float a[12]) {
     PROF_MARK(4)
   }
   PROF_FLUSH
+}
+
+// Both lane halves of a wave hold the same field (lane L and L + 32).  The per-robot phases
+// (drive, integration, walls) run on the half's own robots (lower half 0-2, upper half 3-5), and
+// one v_permlane32_swap per value writes robot k and k + 3 back into every lane's canonical
+// registers; the sequential contacts (robot-robot, ball-robot) and the ball run in both halves
+// on the canonical state.  Same per-robot operations as physics(): bit-identical results with
+// about 28 % fewer VALU instructions per field.
+__device__ __forceinline__ void exch(float v, float& lo, float& hi) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  lo = __uint_as_float(r[0]);  // the lower half's value, in every lane
+  hi = __uint_as_float(r[1]);  // the upper half's value, in every lane
+}
+
+__device__ __forceinline__ void physics_split(Bodies& b, const float a[12]) {
+  const bool up = threadIdx.x >= 32;
+  // this half's robots: own state (o*) is kept across the phases that leave it unchanged
+  float tl[3], tr[3], ox[3], oy[3], ovx[3], ovy[3], ow[3], oqz[3], oqw[3], oc[3], os[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float al = up ? a[2 * k + 6] : a[2 * k], ar = up ? a[2 * k + 7] : a[2 * k + 1];
+    tl[k] = (al * K_WHEEL_RAD_S) * K_WHEEL_R;
+    tr[k] = (ar * K_WHEEL_RAD_S) * K_WHEEL_R;
+    ox[k] = up ? b.x[k + 3] : b.x[k];
+    oy[k] = up ? b.y[k + 3] : b.y[k];
+    ovx[k] = up ? b.vx[k + 3] : b.vx[k];
+    ovy[k] = up ? b.vy[k + 3] : b.vy[k];
+    ow[k] = up ? b.w[k + 3] : b.w[k];
+    oqz[k] = up ? b.qz[k + 3] : b.qz[k];
+    oqw[k] = up ? b.qw[k + 3] : b.qw[k];
+    oc[k] = oqw[k] * oqw[k] - oqz[k] * oqz[k];
+    os[k] = 2.0f * oqw[k] * oqz[k];
+  }
+#pragma unroll 1
+  for (int sub = 0; sub < NSUB; ++sub) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      drive_robot(oc[k], os[k], ovx[k], ovy[k], ow[k], tl[k], tr[k]);
+      integrate_robot(ox[k], oy[k], ovx[k], ovy[k], ow[k], oqz[k], oqw[k], oc[k], os[k]);
+      exch(ox[k], b.x[k], b.x[k + 3]);
+      exch(oy[k], b.y[k], b.y[k + 3]);
+      exch(ovx[k], b.vx[k], b.vx[k + 3]);
+      exch(ovy[k], b.vy[k], b.vy[k + 3]);
+      exch(oc[k], b.c[k], b.c[k + 3]);
+      exch(os[k], b.s[k], b.s[k + 3]);
+    }
+    b.bvx = b.bvx * K_BALL_DAMP;
+    b.bvy = b.bvy * K_BALL_DAMP;
+    b.bx = b.bx + b.bvx * K_H;
+    b.by = b.by + b.bvy * K_H;
+#ifndef VSS_PROF_SKIP_RR
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = i + 1; j < 6; ++j) contact_robot_robot(b, i, j);
+#endif
+#ifndef VSS_PROF_SKIP_BR
+#pragma unroll
+    for (int i = 0; i < 6; ++i) contact_ball_robot(b, i);
+#endif
+#ifndef VSS_PROF_SKIP_WALLS
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      ox[k] = up ? b.x[k + 3] : b.x[k];
+      oy[k] = up ? b.y[k + 3] : b.y[k];
+      ovx[k] = up ? b.vx[k + 3] : b.vx[k];
+      ovy[k] = up ? b.vy[k + 3] : b.vy[k];
+      contact_walls(ox[k], oy[k], ovx[k], ovy[k], K_ROBOT_R);
+      exch(ox[k], b.x[k], b.x[k + 3]);
+      exch(oy[k], b.y[k], b.y[k + 3]);
+      exch(ovx[k], b.vx[k], b.vx[k + 3]);
+      exch(ovy[k], b.vy[k], b.vy[k + 3]);
+    }
+    contact_walls(b.bx, b.by, b.bvx, b.bvy, K_BALL_R);
+#else
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      ox[k] = up ? b.x[k + 3] : b.x[k];
+      oy[k] = up ? b.y[k + 3] : b.y[k];
+      ovx[k] = up ? b.vx[k + 3] : b.vx[k];
+      ovy[k] = up ? b.vy[k + 3] : b.vy[k];
+    }
+#endif
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    exch(ow[k], b.w[k], b.w[k + 3]);
+    exch(oqz[k], b.qz[k], b.qz[k + 3]);
+    exch(oqw[k], b.qw[k], b.qw[k + 3]);
+  }
 }
 
 // ---- state I/O -----------------------------------------------------------------------------------
@@ -623,12 +722,18 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
 
   const int64_t n = args.n;
   const int lane = threadIdx.x;
+  // 32 fields per wave: lanes L and L + 32 hold the same field (physics_split); lanes < 32 own
+  // the field's LDS record and its stores
+  constexpr bool kSplit = 2 * kFpw == kWave;
+  const int fl = kSplit ? (lane & (kFpw - 1)) : lane;
   const int64_t f0 = (int64_t)blockIdx.x * kFpw;
   const int nv = (int)(n - f0 < kFpw ? n - f0 : kFpw);
-  const int64_t f = f0 + lane;
-  const bool valid = lane < nv;
+  const int64_t f = f0 + fl;
+  const bool valid = fl < nv;
+  const bool owner = valid && lane < kFpw;
+  const bool writer = lane < kFpw;  // writes the field's LDS record slots
   const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
-  float* rec = lds + lane * kRec;
+  float* rec = lds + fl * kRec;
   float* orec = lds + lane * obs_rec<A>();  // observation record (lanes < kFpw)
 #if defined(VSS_PROF_PRIO)  // profiling-only experiment: raise half of the waves' issue priority
   if (VSS_PROF_PRIO == 1 ? blockIdx.x < gridDim.x / 2 : (blockIdx.x & 1) != 0) __builtin_amdgcn_s_setprio(3);
@@ -702,7 +807,10 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
 
   // -- gym.simulate replacement ------------------------------------------------------------------------
 #ifndef VSS_PROF_SKIP_PHYSICS  // profiling-only ablation knobs (tools/ablate.py); never set in the product
-  if (valid) physics(b, a);
+  if (valid) {
+    if constexpr (kSplit) physics_split(b, a);
+    else physics(b, a);
+  }
 #endif
 
   // -- post_physics_step: progress, rewards, dones (envs/vss.py:189-265) ----------------------------------
@@ -738,7 +846,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
 
   // -- bookkeeping --------------------------------------------------------------------------------------------
   const uint8_t time_out = (progress >= (int64_t)args.p.max_episode_length - 1) && done != 0;
-  if (valid) {
+  if (owner) {
     store_bodies(args.s.state, n, f, b);
     args.s.progress_buf[f] = progress;
     args.s.reset_buf[f] = done;
@@ -755,14 +863,18 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   }
 
   // dof_velocity_buf (N,12) and, wrapped, the OU action buffer (zeroed for done fields)
+  if (writer) {
 #pragma unroll
-  for (int k = 0; k < 12; ++k) rec[k] = dof[k];
+    for (int k = 0; k < 12; ++k) rec[k] = dof[k];
+  }
   __syncthreads();
   coop_store<12>(args.s.dof_velocity_buf + f0 * 12, nv, lds, lane);
   __syncthreads();
   if constexpr (MODE != VSS_MODE_FULL) {
+    if (writer) {
 #pragma unroll
-    for (int k = 0; k < 12; ++k) rec[k] = done ? ou[k] * 0.0f : ou[k];
+      for (int k = 0; k < 12; ++k) rec[k] = done ? ou[k] * 0.0f : ou[k];
+    }
     __syncthreads();
     coop_store<12>(args.io.ou_buf + f0 * 12, nv, lds, lane);
     __syncthreads();
@@ -770,18 +882,20 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
 
   // rewards
   if constexpr (MODE == VSS_MODE_FULL) {
+    if (writer) {
 #pragma unroll
-    for (int k = 0; k < 24; ++k) rec[k] = rew[k];
+      for (int k = 0; k < 24; ++k) rec[k] = rew[k];
+    }
     __syncthreads();
     coop_store<24>(args.io.rew + f0 * 24, nv, lds, lane);
-    if (valid && args.io.reward_sum) args.io.reward_sum[f] = ((rew[0] + rew[1]) + rew[2]) + rew[3];
+    if (owner && args.io.reward_sum) args.io.reward_sum[f] = ((rew[0] + rew[1]) + rew[2]) + rew[3];
   } else if constexpr (MODE == VSS_MODE_SA) {
-    if (valid) {
+    if (owner) {
       reinterpret_cast<float4*>(args.io.rew)[f] = make_float4(rew[0], rew[1], rew[2], rew[3]);
       args.io.reward_sum[f] = ((rew[0] + rew[1]) + rew[2]) + rew[3];
     }
   } else if constexpr (MODE == VSS_MODE_CMA) {
-    if (valid) {
+    if (owner) {
       float m[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) m[c] = ((rew[c] + rew[4 + c]) + rew[8 + c]) / 3.0f;
@@ -789,11 +903,13 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
       args.io.reward_sum[f] = ((m[0] + m[1]) + m[2]) + m[3];
     }
   } else {
+    if (writer) {
 #pragma unroll
-    for (int k = 0; k < 12; ++k) rec[k] = rew[k];
+      for (int k = 0; k < 12; ++k) rec[k] = rew[k];
+    }
     __syncthreads();
     coop_store<12>(args.io.rew + f0 * 12, nv, lds, lane);
-    if (valid) {
+    if (owner) {
 #pragma unroll
       for (int ag = 0; ag < 3; ++ag)
         args.io.reward_sum[f * 3 + ag] = ((rew[4 * ag] + rew[4 * ag + 1]) + rew[4 * ag + 2]) + rew[4 * ag + 3];
@@ -840,12 +956,16 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
   __shared__ float lds[kWave * kRec];
   const int64_t n = args.n;
   const int lane = threadIdx.x;
+  constexpr bool kSplit = 2 * kFpwRollout == kWave;  // lanes L and L + 32 hold the same field
+  const int fl = kSplit ? (lane & (kFpwRollout - 1)) : lane;
   const int64_t f0 = (int64_t)blockIdx.x * kFpwRollout;
   const int nv = (int)(n - f0 < kFpwRollout ? n - f0 : kFpwRollout);
-  const int64_t f = f0 + lane;
-  const bool valid = lane < nv;
+  const int64_t f = f0 + fl;
+  const bool valid = fl < nv;  // both halves carry the state (and apply resets) across steps
+  const bool owner = valid && lane < kFpwRollout;
+  const bool writer = lane < kFpwRollout;
   const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
-  float* rec = lds + lane * kRec;
+  float* rec = lds + fl * kRec;
   float* orec = lds + lane * kRecObs6;  // observation record (lanes < kFpwRollout)
 
   int64_t progress = 0, reset_prev = 0;
@@ -877,7 +997,10 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
     float pbx = b.bx, pby = b.by, prx[6], pry[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) { prx[i] = b.x[i]; pry[i] = b.y[i]; }
-    if (valid) physics(b, a);
+    if (valid) {
+      if constexpr (kSplit) physics_split(b, a);
+      else physics(b, a);
+    }
     progress += 1;
     float rew[24];
     done = rewards_and_done(args.p, b, pbx, pby, prx, pry, a, progress, rew);
@@ -897,12 +1020,14 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
     __syncthreads();
     coop_store_obs<6>(args.io.obs + (step_off + f0) * 312, nv, lds, lane);
     __syncthreads();
+    if (writer) {
 #pragma unroll
-    for (int i = 0; i < 24; ++i) rec[i] = rew[i];
+      for (int i = 0; i < 24; ++i) rec[i] = rew[i];
+    }
     __syncthreads();
     coop_store<24>(args.io.rew + (step_off + f0) * 24, nv, lds, lane);
     __syncthreads();
-    if (valid) {
+    if (owner) {
       args.io.dones[step_off + f] = done;
       args.io.time_outs[step_off + f] = (progress >= (int64_t)args.p.max_episode_length - 1) && done != 0;
       args.io.progress_f[step_off + f] = (float)progress;
@@ -910,14 +1035,16 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
     reset_prev = done;
   }
 
-  if (valid) {
+  if (owner) {
     store_bodies(args.s.state, n, f, b);
     args.s.progress_buf[f] = progress;
     args.s.reset_buf[f] = done;
     args.s.rng_counter[f] = ctr + (uint32_t)args.k_steps;
   }
+  if (writer) {
 #pragma unroll
-  for (int i = 0; i < 12; ++i) rec[i] = dof[i];
+    for (int i = 0; i < 12; ++i) rec[i] = dof[i];
+  }
   __syncthreads();
   coop_store<12>(args.s.dof_velocity_buf + f0 * 12, nv, lds, lane);
 }

@@ -735,9 +735,6 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
   float* rec = lds + fl * kRec;
   float* orec = lds + lane * obs_rec<A>();  // observation record (lanes < kFpw)
-#if defined(VSS_PROF_PRIO)  // profiling-only experiment: raise half of the waves' issue priority
-  if (VSS_PROF_PRIO == 1 ? blockIdx.x < gridDim.x / 2 : (blockIdx.x & 1) != 0) __builtin_amdgcn_s_setprio(3);
-#endif
 
   // -- state loads first (46 coalesced channel loads in flight), then the action transpose -------
   int64_t progress = 0, reset_prev = 0;

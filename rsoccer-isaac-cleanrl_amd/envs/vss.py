@@ -154,21 +154,42 @@ class VSS:
         return self.act_space
 
     # ------------------------------------------------------------------------------ the step
+    def _check_buffer(self, name: str, t, numel: int, dtype: torch.dtype, required: bool = True):
+        """A caller buffer the kernel writes: right size, dtype, device, contiguous (the kernel
+        trusts its pointers, so a short buffer would be an out-of-bounds device write)."""
+        if t is None:
+            if required:
+                raise ValueError(f"{name} is required")
+            return
+        if t.numel() != numel or t.dtype != dtype or t.device != self.device or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous {dtype} tensor of {numel} elements on {self.device}, "
+                             f"got {tuple(t.shape)} {t.dtype} on {t.device}")
+
     def native_step(self, mode: int, actions: torch.Tensor, io: dict) -> None:
         """One fused step in `mode` (FULL / SA / CMA / DMA) writing into the tensors of `io`.
 
-        Buffers are checked here (shape, dtype, device, contiguity); the kernel itself is one
+        Buffers are checked here (size, dtype, device, contiguity); the kernel itself is one
         launch on the current stream with no host synchronisation."""
         n = self.num_fields
-        rows = {N.MODE_FULL: n, N.MODE_SA: n, N.MODE_CMA: n, N.MODE_DMA: 3 * n}[mode]
+        if mode not in (N.MODE_FULL, N.MODE_SA, N.MODE_CMA, N.MODE_DMA):
+            raise ValueError(f"unknown mode {mode}")
+        rows = {N.MODE_FULL: n, N.MODE_SA: n, N.MODE_CMA: n, N.MODE_DMA: 3 * n}[mode]   # output rows
         width = {N.MODE_FULL: 12, N.MODE_SA: 2, N.MODE_CMA: 6, N.MODE_DMA: 2}[mode]
+        agents = {N.MODE_FULL: 6, N.MODE_SA: 1, N.MODE_CMA: 1, N.MODE_DMA: 3}[mode]     # obs rows per field
         if actions.numel() != rows * width:
             raise ValueError(f"actions must have {rows * width} elements, got {tuple(actions.shape)}")
         if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():
             actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
-        for k, t in io.items():
-            if t is not None and (t.device != self.device or not t.is_contiguous()):
-                raise ValueError(f"io[{k}] must be a contiguous tensor on {self.device}")
+        full = mode == N.MODE_FULL
+        r = 1 if full else rows  # time_outs / progress rows: per field, or per agent row for DMA
+        self._check_buffer("io['obs']", io.get("obs"), n * agents * 52, torch.float32)
+        self._check_buffer("io['terminal_obs']", io.get("terminal_obs"), n * agents * 52, torch.float32)
+        self._check_buffer("io['rew']", io.get("rew"), n * 24 if full else rows * 4, torch.float32)
+        self._check_buffer("io['reward_sum']", io.get("reward_sum"), rows, torch.float32, required=not full)
+        self._check_buffer("io['ou_buf']", io.get("ou_buf"), n * 12, torch.float32, required=not full)
+        self._check_buffer("io['dones_rep']", io.get("dones_rep"), rows, torch.long, required=mode == N.MODE_DMA)
+        self._check_buffer("io['time_outs']", io.get("time_outs"), n if full else r, torch.bool)
+        self._check_buffer("io['progress_f']", io.get("progress_f"), n if full else r, torch.float32)
         cio = N.VssStepIO(actions.data_ptr(), N.ptr(io.get("ou_buf")), N.ptr(io["obs"]),
                           N.ptr(io["terminal_obs"]), N.ptr(io["rew"]), N.ptr(io.get("reward_sum")),
                           N.ptr(io.get("dones_rep")), N.ptr(io["time_outs"]), N.ptr(io["progress_f"]))
@@ -199,6 +220,11 @@ class VSS:
         if actions.numel() != K * n * 12:
             raise ValueError(f"actions must be (K, {n}, 2, 3, 2), got {tuple(actions.shape)}")
         actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        if out is not None:
+            for k, (numel, dt) in dict(obs=(K * n * 312, torch.float32), terminal_observation=(K * n * 312, torch.float32),
+                                       rew=(K * n * 24, torch.float32), dones=(K * n, torch.long),
+                                       time_outs=(K * n, torch.bool), progress_buffer=(K * n, torch.float32)).items():
+                self._check_buffer(f"out['{k}']", out.get(k), numel, dt)
         if out is None:
             dev = self.device
             out = dict(obs=torch.empty((K, n, 2, 3, 52), device=dev),
@@ -235,7 +261,10 @@ class VSS:
 
     def compute_observations(self, out: torch.Tensor | None = None, n_agents: int = 6):
         """compute_obs (envs/vss.py:205-216, 530-575) into `obs_buf` (or `out`)."""
+        if n_agents not in (1, 3, 6):
+            raise ValueError("n_agents must be 1 (blue robot 0), 3 (blue team) or 6 (both teams)")
         out = self.obs_buf if out is None else out
+        self._check_buffer("out", out, self.num_fields * n_agents * 52, torch.float32)
         st = self._c_state()
         rc = N.load().vss_compute_observations(N.stream_of(self.device), self.num_fields, N.ctypes.byref(st),
                                                out.data_ptr(), n_agents)

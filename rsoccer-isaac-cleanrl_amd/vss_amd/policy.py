@@ -32,6 +32,7 @@ class FusedPolicy:
         self._critic = torch.empty(lib.vss_mlp_packed_size(1), device=self.device)
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.counter = 0
+        self._keep = {}
         self.refresh()
 
     @staticmethod
@@ -40,11 +41,12 @@ class FusedPolicy:
 
     def _pack(self, seq, n_out, out):
         lins = self._linears(seq)
-        if len(lins) != 5:
-            raise ValueError("expected the reference Agent's 5-layer MLPs")
-        ws = [l.weight.detach().contiguous() for l in lins]
-        bs = [l.bias.detach().contiguous() for l in lins]
-        self._keep = ws + bs
+        dims = [52, 256, 512, 512, 256, n_out]
+        if len(lins) != 5 or any((l.in_features, l.out_features) != (dims[i], dims[i + 1]) for i, l in enumerate(lins)):
+            raise ValueError(f"expected the reference Agent's MLP {' -> '.join(map(str, dims))}")
+        ws = [l.weight.detach().to(self.device, torch.float32).contiguous() for l in lins]
+        bs = [l.bias.detach().to(self.device, torch.float32).contiguous() for l in lins]
+        self._keep[n_out] = ws + bs  # alive until the (asynchronous) pack has read them
         wa = (ctypes.c_void_p * 5)(*[w.data_ptr() for w in ws])
         ba = (ctypes.c_void_p * 5)(*[b.data_ptr() for b in bs])
         N.check(N.load().vss_mlp_pack(N.stream_of(self.device), n_out, wa, ba, out.data_ptr()), "vss_mlp_pack")
@@ -70,6 +72,8 @@ class FusedPolicy:
             mean = torch.empty((rows, self.n_act), device=dev)
             if action is not None:
                 action = action.to(dev, torch.float32).contiguous()
+                if action.numel() != rows * self.n_act:
+                    raise ValueError(f"action must have {rows} x {self.n_act} elements, got {tuple(action.shape)}")
             outs = [act_out, logp, ent, mean]
         self.counter += 1
         rc = N.load().vss_policy_forward(
@@ -94,15 +98,14 @@ class FusedPolicy:
     def get_value_masked(self, obs, mask: torch.Tensor, out: torch.Tensor):
         """critic(obs) written into `out` (rows, 1) only for rows with mask != 0 (int64 mask,
         e.g. the env's dones); other rows of `out` are left untouched."""
-        obs = obs.reshape(-1, 52)
+        obs = obs.reshape(-1, 52).to(self.device, torch.float32).contiguous()
         rows = obs.shape[0]
-        if mask.dtype != torch.long:
-            mask = mask.long()
-        mask = mask.contiguous()
-        if out.numel() != rows or not out.is_contiguous() or mask.numel() != rows:
-            raise ValueError("out / mask must have one element per row")
+        mask = mask.to(self.device, torch.long).contiguous()
+        if (out.numel() != rows or out.dtype != torch.float32 or out.device != self.device
+                or not out.is_contiguous() or mask.numel() != rows):
+            raise ValueError("out (float32, contiguous, on the policy's device) and mask need one element per row")
         rc = N.load().vss_value_forward_masked(
-            N.stream_of(self.device), rows, self.n_act, obs.contiguous().data_ptr(), None, None,
+            N.stream_of(self.device), rows, self.n_act, obs.data_ptr(), None, None,
             self._critic.data_ptr(), self.seed, 0, None, None, None, None, out.data_ptr(), None, mask.data_ptr())
         N.check(rc, "vss_value_forward_masked")
         return out

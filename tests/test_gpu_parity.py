@@ -267,6 +267,39 @@ def test_zero_fields_is_a_noop():
     assert torch.equal(before, env.state)
 
 
+def test_host_layer_rejects_bad_buffers_before_launch():
+    """The kernels trust their pointers, so the env layer checks every caller buffer (size,
+    dtype, device, contiguity) and raises before launching; the state is left untouched."""
+    n = 64
+    env = make_vss(n)
+    before = env.state.clone()
+    acts = torch.zeros((n, 2, 3, 2), device=DEV)
+    good = dict(obs=env.obs_buf, terminal_obs=env.terminal_obs_buf, rew=env.rew_buf, reward_sum=None,
+                time_outs=env.timeout_buf, progress_f=env.progress_f_buf)
+    bad = [dict(good, obs=torch.zeros((n - 1, 2, 3, 52), device=DEV)),          # short
+           dict(good, rew=torch.zeros((n, 2, 3, 4), device=DEV, dtype=torch.float64)),  # dtype
+           dict(good, time_outs=torch.zeros(n, device=DEV)),                          # float, not bool
+           dict(good, terminal_obs=torch.zeros((n, 2, 3, 104), device=DEV)[..., ::2]),  # strided
+           dict(good, progress_f=torch.zeros(n))]                                     # host memory
+    for io in bad:
+        with pytest.raises(ValueError):
+            env.native_step(N.MODE_FULL, acts, io)
+    with pytest.raises(ValueError):  # wrapped modes need the OU buffer and reward_sum
+        env.native_step(N.MODE_SA, torch.zeros((n, 2), device=DEV), dict(good, obs=torch.zeros((n, 52), device=DEV)))
+    with pytest.raises(ValueError):
+        env.native_step(N.MODE_FULL, torch.zeros((n + 1, 12), device=DEV), good)
+    with pytest.raises(ValueError):
+        env.rollout(torch.zeros((4, n, 2, 3, 2), device=DEV), out=dict(
+            obs=torch.zeros((3, n, 2, 3, 52), device=DEV)))
+    with pytest.raises(ValueError):
+        env.compute_observations(out=torch.zeros((n, 52), device=DEV), n_agents=3)
+    with pytest.raises(ValueError):
+        env.compute_observations(n_agents=2)
+    torch.cuda.synchronize()
+    assert torch.equal(before, env.state)
+    env.native_step(N.MODE_FULL, acts, good)  # and the good set still steps
+
+
 @pytest.mark.parametrize("n,K", [(4096, 24), (65, 50)])
 def test_rollout_equals_sequential_steps_and_oracle(n, K):
     """vss_rollout (K steps per launch) == K vss_step launches == K oracle steps, bit for bit."""

@@ -97,3 +97,26 @@ def test_masked_terminal_values_write_only_masked_rows():
     out0 = torch.full((rows, 1), 7.0, device=DEV)
     fused.get_value_masked(obs, torch.zeros_like(mask), out0)
     assert torch.all(out0 == 7.0)
+
+
+def test_rejects_bad_shapes_before_launch():
+    """The kernels trust their pointers: a network of the wrong shape, a short action or output
+    buffer, or an output in the wrong dtype is refused on the host."""
+    from vss_amd.policy import FusedPolicy
+    agent = make_agent(2, 6)
+    wrong = make_agent(2, 6)
+    wrong.critic[2] = torch.nn.Linear(256, 500).to(DEV)
+    with pytest.raises(ValueError):
+        FusedPolicy(wrong)
+    fused = FusedPolicy(agent)
+    obs = torch.randn(64, 52, device=DEV)
+    with pytest.raises(ValueError):
+        fused.get_action_and_value(obs, torch.zeros(63, 2, device=DEV))
+    mask = torch.ones(64, dtype=torch.long, device=DEV)
+    with pytest.raises(ValueError):
+        fused.get_value_masked(obs, mask, torch.zeros(63, 1, device=DEV))
+    with pytest.raises(ValueError):
+        fused.get_value_masked(obs, mask, torch.zeros(64, 1, device=DEV, dtype=torch.float64))
+    out = torch.zeros(64, 1, device=DEV)
+    fused.get_value_masked(obs, mask.bool(), out)  # a bool mask (the env's dones) is accepted
+    assert torch.equal(out, fused.get_value(obs))

@@ -62,9 +62,14 @@ extern "C" {
 #define VSS_MODE_CMA 2   /* CMA: learner = blue team, one 6-vector (envs/wrappers.py:118-148) */
 #define VSS_MODE_DMA 3   /* DMA: learner = blue robots 0..2, one row each (wrappers.py:151-180) */
 
+/* Alignment (checked; VSS_E_ARG otherwise): observation, reward, dof_velocity, OU and FULL /
+ * rollout action buffers 16 B (float4 access); SA/CMA/DMA action buffers 8 B; int64 buffers 8 B;
+ * packed MLP weights 16 B.  Allocator (hipMalloc / torch) pointers always qualify; a view at an
+ * odd element offset may not. */
+
 /* error codes */
 #define VSS_OK 0
-#define VSS_E_ARG 1      /* null pointer / bad size / bad mode */
+#define VSS_E_ARG 1      /* null or misaligned pointer / bad size / bad mode */
 #define VSS_E_LAUNCH 2   /* kernel launch failed (hipGetLastError) */
 
 typedef struct vss_params {

@@ -308,7 +308,8 @@ int64_t vss_mlp_packed_size(int32_t n_out) {
 }
 
 int vss_mlp_pack(void* stream, int32_t n_out, const float* const* weights, const float* const* biases, float* packed) {
-  if (n_out < 1 || n_out > 8 || !weights || !biases || !packed) return VSS_E_ARG;
+  if (n_out < 1 || n_out > 8 || !weights || !biases || !packed || (reinterpret_cast<uintptr_t>(packed) & 15))
+    return VSS_E_ARG;
   for (int i = 0; i < 5; ++i)
     if (!weights[i] || !biases[i]) return VSS_E_ARG;
   hipLaunchKernelGGL(vpol::pack_kernel, dim3(1024), dim3(256), 0, (hipStream_t)stream, n_out, weights[0], biases[0],
@@ -328,7 +329,11 @@ int vss_value_forward_masked(void* stream, int64_t rows, int32_t n_act, const fl
                              const float* logstd, const float* critic_packed, uint64_t seed, uint64_t counter,
                              const float* action_in, float* action_out, float* logprob_out, float* entropy_out,
                              float* value_out, float* mean_out, const int64_t* row_mask) {
-  if (rows < 0 || !obs || !critic_packed) return VSS_E_ARG;
+  // packed weights are read as float4 (16-B aligned), the mask as int64
+  auto misaligned = [](const void* ptr, uintptr_t al) { return (reinterpret_cast<uintptr_t>(ptr) & (al - 1)) != 0; };
+  if (rows < 0 || !obs || !critic_packed || misaligned(critic_packed, 16) || misaligned(actor_packed, 16) ||
+      misaligned(row_mask, 8))
+    return VSS_E_ARG;
   const bool critic_only = actor_packed == nullptr;
   if (!critic_only && (!logstd || !(n_act == 2 || n_act == 6))) return VSS_E_ARG;
   if (row_mask && !critic_only) return VSS_E_ARG;

@@ -1107,15 +1107,20 @@ int vss_prof_read(unsigned long long* host_out) {
 const char* vss_error_string(int code) {
   switch (code) {
     case VSS_OK: return "ok";
-    case VSS_E_ARG: return "invalid argument (null buffer, bad size or bad mode)";
+    case VSS_E_ARG: return "invalid argument (null or misaligned buffer, bad size or bad mode)";
     case VSS_E_LAUNCH: return "kernel launch failed";
     default: return "unknown error";
   }
 }
 
+// Null or misaligned: the kernels move float4 / float2 vectors and int64 scalars.
+static bool bad(const void* ptr, uintptr_t align) { return !ptr || (reinterpret_cast<uintptr_t>(ptr) & (align - 1)); }
+static bool misaligned(const void* ptr, uintptr_t align) { return ptr && (reinterpret_cast<uintptr_t>(ptr) & (align - 1)); }
+
 static int check_state(int64_t n, const vss_state* st) {
   if (n < 0 || n > (int64_t(1) << 26) || !st) return VSS_E_ARG;
-  if (!st->state || !st->progress_buf || !st->reset_buf || !st->dof_velocity_buf || !st->rng_counter)
+  if (bad(st->state, 4) || bad(st->progress_buf, 8) || bad(st->reset_buf, 8) || bad(st->dof_velocity_buf, 16) ||
+      bad(st->rng_counter, 4))
     return VSS_E_ARG;
   return VSS_OK;
 }
@@ -1126,7 +1131,9 @@ int vss_step(void* stream, int64_t n, int32_t mode, const vss_params* p, const v
              const vss_step_io* io) {
   if (int rc = check_state(n, st)) return rc;
   if (!p || !io || mode < VSS_MODE_FULL || mode > VSS_MODE_DMA) return VSS_E_ARG;
-  if (!io->actions || !io->obs || !io->terminal_obs || !io->rew || !io->time_outs || !io->progress_f)
+  if (bad(io->actions, mode == VSS_MODE_FULL ? 16 : 8) || bad(io->obs, 16) || bad(io->terminal_obs, 16) ||
+      bad(io->rew, 16) || bad(io->time_outs, 1) || bad(io->progress_f, 4) || misaligned(io->reward_sum, 4) ||
+      misaligned(io->ou_buf, 16) || misaligned(io->dones_rep, 8))
     return VSS_E_ARG;
   if (mode != VSS_MODE_FULL && (!io->ou_buf || !io->reward_sum)) return VSS_E_ARG;
   if (mode == VSS_MODE_DMA && !io->dones_rep) return VSS_E_ARG;
@@ -1150,7 +1157,8 @@ int vss_rollout(void* stream, int64_t n, int32_t k_steps, const vss_params* p, c
                 const vss_rollout_io* io) {
   if (int rc = check_state(n, st)) return rc;
   if (!p || !io || k_steps < 1 || k_steps > (1 << 20)) return VSS_E_ARG;
-  if (!io->actions || !io->obs || !io->terminal_obs || !io->rew || !io->dones || !io->time_outs || !io->progress_f)
+  if (bad(io->actions, 16) || bad(io->obs, 16) || bad(io->terminal_obs, 16) || bad(io->rew, 16) ||
+      bad(io->dones, 8) || bad(io->time_outs, 1) || bad(io->progress_f, 4))
     return VSS_E_ARG;
   if (n == 0) return VSS_OK;
   vss::RolloutArgs args{n, k_steps, *p, *st, *io};
@@ -1170,7 +1178,7 @@ int vss_reset_dones(void* stream, int64_t n, const vss_params* p, const vss_stat
 
 int vss_compute_observations(void* stream, int64_t n, const vss_state* st, float* obs, int32_t n_agents) {
   if (int rc = check_state(n, st)) return rc;
-  if (!obs || !(n_agents == 1 || n_agents == 3 || n_agents == 6)) return VSS_E_ARG;
+  if (bad(obs, 16) || !(n_agents == 1 || n_agents == 3 || n_agents == 6)) return VSS_E_ARG;
   if (n == 0) return VSS_OK;
   const dim3 grid((unsigned)((n + vss::kWave - 1) / vss::kWave)), block(vss::kWave);
   hipStream_t s = (hipStream_t)stream;

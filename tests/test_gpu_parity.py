@@ -267,6 +267,25 @@ def test_zero_fields_is_a_noop():
     assert torch.equal(before, env.state)
 
 
+def test_c_abi_rejects_misaligned_vector_buffers():
+    """Straight through the C ABI: an obs or action pointer 4 B off its 16-B alignment is refused
+    with VSS_E_ARG (the kernels move float4 vectors), the aligned call succeeds."""
+    lib = N.load()
+    env = make_vss(64)
+    prm, st = env._c_params(), env._c_state()
+    acts = torch.zeros(64 * 12 + 4, device=DEV)
+    obs = torch.zeros(64 * 312 + 4, device=DEV)
+
+    def call(a_off, o_off):
+        io = N.VssStepIO(acts.data_ptr() + a_off, None, obs.data_ptr() + o_off, env.terminal_obs_buf.data_ptr(),
+                         env.rew_buf.data_ptr(), None, None, env.timeout_buf.data_ptr(), env.progress_f_buf.data_ptr())
+        return lib.vss_step(N.stream_of(env.device), 64, 0, N.ctypes.byref(prm), N.ctypes.byref(st), N.ctypes.byref(io))
+
+    assert call(0, 4) == 1 and call(4, 0) == 1 and call(8, 0) == 1
+    assert call(0, 0) == 0
+    torch.cuda.synchronize()
+
+
 def test_host_layer_rejects_bad_buffers_before_launch():
     """The kernels trust their pointers, so the env layer checks every caller buffer (size,
     dtype, device, contiguity) and raises before launching; the state is left untouched."""

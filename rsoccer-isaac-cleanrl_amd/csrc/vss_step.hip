@@ -717,21 +717,22 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   constexpr int R = MODE == VSS_MODE_DMA ? 3 : 1;
   constexpr int NL = MODE == VSS_MODE_SA ? 2 : 6;  // learner action floats per field
   constexpr int kFpw = fields_per_wave<MODE>();
-  static_assert(kFpw * obs_rec<A>() <= kWave * kRec, "observation records must fit the LDS block");
-  __shared__ float lds[kWave * kRec];
+  // <= 32 fields per wave: lanes L and L + 32 hold field L (physics_split); lanes < 32 address the
+  // LDS records, so LDS holds 32 plain records or kFpw observation records, whichever is larger
+  constexpr bool kSplit = 2 * kFpw <= kWave;
+  constexpr int kLds = kSplit ? (32 * kRec > kFpw * obs_rec<A>() ? 32 * kRec : kFpw * obs_rec<A>()) : kWave * kRec;
+  static_assert(kFpw * obs_rec<A>() <= kLds, "observation records must fit the LDS block");
+  __shared__ float lds[kLds];
 
   const int64_t n = args.n;
   const int lane = threadIdx.x;
-  // 32 fields per wave: lanes L and L + 32 hold the same field (physics_split); lanes < 32 own
-  // the field's LDS record and its stores
-  constexpr bool kSplit = 2 * kFpw == kWave;
-  const int fl = kSplit ? (lane & (kFpw - 1)) : lane;
+  const int fl = kSplit ? (lane & 31) : lane;  // this lane's field within the wave
   const int64_t f0 = (int64_t)blockIdx.x * kFpw;
   const int nv = (int)(n - f0 < kFpw ? n - f0 : kFpw);
   const int64_t f = f0 + fl;
   const bool valid = fl < nv;
-  const bool owner = valid && lane < kFpw;
-  const bool writer = lane < kFpw;  // writes the field's LDS record slots
+  const bool owner = valid && (!kSplit || lane < 32);  // stores the field's outputs
+  const bool writer = !kSplit || lane < 32;            // writes the field's LDS record slots
   const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
   float* rec = lds + fl * kRec;
   float* orec = lds + lane * obs_rec<A>();  // observation record (lanes < kFpw)

@@ -12,14 +12,13 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
 import torch
 
 from vss_amd import _native as N
 
 from ._gym import Box, Wrapper
 from .vss import VSS, default_cfg
-
-import numpy as np
 
 
 def random_ou(prev: torch.Tensor) -> torch.Tensor:

@@ -170,14 +170,44 @@ class _NullWriter:
         pass
 
 
+class _CsvWriter:
+    """The SummaryWriter calls the loop makes, appended to `<run>/scalars.csv` (tag,value,step)
+    when TensorBoard is not installed, so the learning curves are kept either way."""
+
+    def __init__(self, path):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        self._f = open(path, "w")
+        self._f.write("tag,value,step\n")
+
+    def add_scalar(self, tag, value, step):
+        self._f.write(f"{tag},{float(value)!r},{int(step)}\n")
+
+    def add_text(self, *a, **k):
+        pass
+
+    def close(self):
+        self._f.close()
+
+
 def make_writer(args, run_name, rank):
     if rank != 0 or not args.log:
         return _NullWriter()
     try:
         from torch.utils.tensorboard import SummaryWriter
         return SummaryWriter(f"{args.save_path}/{run_name}")
-    except Exception:  # tensorboard not installed
-        return _NullWriter()
+    except ImportError:  # tensorboard not installed
+        return _CsvWriter(f"{args.save_path}/{run_name}/scalars.csv")
+
+
+EP_KEYS = ("goal", "grad", "move", "energy", "return")  # info['r'] keys (envs/wrappers.py:74-80)
+
+
+def first_done_stats(done: torch.Tensor, info: dict) -> torch.Tensor:
+    """[any done, goal, grad, move, energy, return, length] of the FIRST env with done set — what
+    ppo…:273-279 logs by looping over the envs on the host — as one device tensor, no sync."""
+    d = done.float()
+    idx = torch.argmax(d)  # index of the first maximum
+    return torch.stack([d.max()] + [info["r"][k][idx].float() for k in EP_KEYS] + [info["l"][idx].float()])
 
 
 def compute_gae(rewards, values, next_values, next_dones, next_timeouts, gamma, lam):
@@ -327,6 +357,10 @@ def train(args):
         t_roll = time.time()
         ep_ret = torch.zeros((), device=device)
         ep_cnt = torch.zeros((), device=device)
+        # ppo…:273-279 logs the first finished env's episode stats at steps 0-2 (a host-sync loop);
+        # here: [any done, goal, grad, move, energy, return, length] on the device, read once below
+        ep_first = torch.zeros((3, 7), device=device)
+        step0 = global_step
         if fused is not None:
             fused.refresh()  # weights changed in the last update
         for step in range(T):
@@ -353,6 +387,8 @@ def train(args):
             d = next_done.float()
             ep_ret += (info["r"]["return"] * d).sum()
             ep_cnt += d.sum()
+            if step <= 2:
+                ep_first[step] = first_done_stats(d, info)
         if fused is not None:
             v_last = fused.get_value(next_obs).view(1, E)
             nxt = torch.cat([values[1:], v_last], 0)
@@ -360,6 +396,13 @@ def train(args):
         if device.type == "cuda":
             torch.cuda.synchronize()
         t_roll = time.time() - t_roll
+        if rank == 0 and args.log:
+            for t, row in enumerate(ep_first.tolist()):
+                if row[0] > 0:
+                    gs = step0 + (t + 1) * E * world
+                    for k, v in zip(EP_KEYS, row[1:6]):
+                        writer.add_scalar(f"rws/episodic_{k}", v, gs)
+                    writer.add_scalar("rws/episodic_length", row[6], gs)
 
         with torch.no_grad():
             advantages, returns = compute_gae(rewards, values, next_values, next_dones, next_timeouts,
@@ -376,8 +419,9 @@ def train(args):
                "episodes": float(ep_cnt), "mean_return": float(ep_ret / ep_cnt.clamp(min=1)),
                **{k: float(v) for k, v in stats.items()}}
         history.append(rec)
-        for k in ("v_loss", "pg_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac"):
-            writer.add_scalar(f"losses/{k if k != 'v_loss' else 'value_loss'}", rec[k], global_step)
+        for k, name in (("v_loss", "value_loss"), ("pg_loss", "policy_loss"), ("entropy", "entropy"),
+                        ("old_approx_kl", "old_approx_kl"), ("approx_kl", "approx_kl"), ("clipfrac", "clipfrac")):
+            writer.add_scalar(f"losses/{name}", rec[k], global_step)
         writer.add_scalar("losses/learning_rate", optimizer.param_groups[0]["lr"], global_step)
         writer.add_scalar("Charts/SPS", sps, global_step)
         if rank == 0 and args.log:

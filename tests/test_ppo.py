@@ -173,7 +173,12 @@ def test_train_end_to_end_gpu(env_id, tmp_path):
         for k in ("v_loss", "pg_loss", "entropy", "approx_kl"):
             assert np.isfinite(h[k]), (k, h)
         assert h["sps"] > 0
-    assert os.path.exists(os.path.join(tmp_path, f"{args.exp_name}_ppo-{env_id}_1", f"{args.exp_name}_ppo-{env_id}_1-agent.pt"))
+    run = os.path.join(tmp_path, f"{args.exp_name}_ppo-{env_id}_1")
+    assert os.path.exists(os.path.join(run, f"{args.exp_name}_ppo-{env_id}_1-agent.pt"))
+    if os.path.exists(os.path.join(run, "scalars.csv")):  # no TensorBoard: the CSV fallback
+        tags = {line.split(",")[0] for line in open(os.path.join(run, "scalars.csv")).read().splitlines()[1:]}
+        assert {"losses/value_loss", "losses/policy_loss", "losses/entropy", "losses/approx_kl",
+                "losses/clipfrac", "losses/learning_rate", "Charts/SPS"} <= tags
 
 
 @pytest.mark.gpu
@@ -210,3 +215,31 @@ def test_fused_rollout_next_values_equal_reference_definition(tmp_path):
     nv = torch.where(dones.bool(), term, torch.cat([values[1:], v_last], 0))
     assert dones.sum() > 0
     assert torch.equal(nv, full)
+
+
+def test_csv_writer_fallback(tmp_path):
+    w = P._CsvWriter(os.path.join(tmp_path, "run", "scalars.csv"))
+    w.add_scalar("losses/value_loss", 0.5, 10)
+    w.add_scalar("rws/episodic_return", torch.tensor(-1.25), 20)
+    w.close()
+    lines = open(os.path.join(tmp_path, "run", "scalars.csv")).read().splitlines()
+    assert lines == ["tag,value,step", "losses/value_loss,0.5,10", "rws/episodic_return,-1.25,20"]
+
+
+@pytest.mark.parametrize("done_idx", [[], [0], [5, 9], [11]])
+def test_first_done_stats_matches_reference_loop(done_idx):
+    """Same env as the reference's `for idx, d in enumerate(next_done): if d: ... break`."""
+    g = torch.Generator().manual_seed(3)
+    n = 12
+    done = torch.zeros(n, dtype=torch.long)
+    done[done_idx] = 1
+    r = torch.randn(n, 4, generator=g)
+    info = {"r": {"goal": r[:, 0], "grad": r[:, 1], "move": r[:, 2], "energy": r[:, 3], "return": r.sum(1)},
+            "l": torch.randint(1, 400, (n,), generator=g, dtype=torch.int32)}
+    got = P.first_done_stats(done, info)
+    want = [0.0] * 7
+    for idx, d in enumerate(done):
+        if d:
+            want = [1.0] + [float(info["r"][k][idx]) for k in P.EP_KEYS] + [float(info["l"][idx])]
+            break
+    assert got.tolist() == pytest.approx(want) if done_idx else got[0] == 0

@@ -99,79 +99,110 @@ __device__ __forceinline__ float fast_tanh(float x) {
 
 // ---- one MFMA layer: hout = tanh(W . hin + b), all in registers ------------------------------------
 // The 4 waves of a workgroup (64 rows) share every weight chunk through LDS: a chunk = CK
-// k-steps x N outputs (CK * N * 4 floats = 32 KB at N = 512), double-buffered.  Each wave loads
-// a quarter of chunk c+1 from L2 into registers while it runs the MFMAs of chunk c out of LDS,
-// then writes it to the other LDS buffer; one workgroup barrier per chunk.  L2 weight traffic
-// is 1/4 of the per-wave streaming form.  All loops are unrolled (hin / acc indices static).
-constexpr int kCK = 4;                       // k-steps per chunk
-constexpr int kChunkFloats = kCK * kH2 * 4;  // largest chunk (N = 512): 8192 floats = 32 KB
+// k-steps x (N / OS) outputs, double-buffered.  Each wave loads a quarter of chunk c+1 from L2
+// into registers while it runs the MFMAs of chunk c out of LDS, then writes it to the other LDS
+// buffer; one workgroup barrier per chunk.  L2 weight traffic is 1/4 of the per-wave streaming
+// form.  OS > 1 computes the outputs in OS passes of N / OS (each weight is still read once; the
+// inputs stay in registers): OS x fewer live accumulators, which is what keeps the 512-wide layers
+// out of scratch.  All loops are unrolled (hin / acc indices static).
+#ifndef VPOL_CK
+#define VPOL_CK 8
+#endif
+#ifndef VPOL_OS
+#define VPOL_OS 2
+#endif
+constexpr int kCK = VPOL_CK;                               // k-steps per chunk
+constexpr int kOS512 = VPOL_OS;                            // output passes of the 512-wide layers
+constexpr int kChunkFloats = kCK * (kH2 / kOS512 > kH1 ? kH2 / kOS512 : kH1) * 4;  // largest chunk (floats)
 
-template <int K4, int NT>
+template <int K4, int NT, int OS>
 __device__ __forceinline__ void mfma_layer(const float* __restrict__ wp, const float* __restrict__ bias,
                                            const float (&hin)[K4], float (&hout)[NT * 4], int lane,
                                            float* __restrict__ lds, int wave) {
-  constexpr int NQ = NT / 4;                         // float4 weight groups per k-step
-  constexpr int NCH = (K4 + kCK - 1) / kCK;          // chunks in this layer
-  constexpr int CH_F4 = kCK * NQ * 64;               // float4 per full chunk
+  static_assert(NT % (4 * OS) == 0, "passes must split whole float4 groups");
+  constexpr int NQ = NT / 4;                         // float4 weight groups per k-step (layer)
+  constexpr int NTP = NT / OS, NQP = NQ / OS;        // tiles / groups per pass
+  constexpr int NCH = (K4 + kCK - 1) / kCK;          // chunks per pass
+  constexpr int CH_F4 = kCK * NQP * 64;              // float4 per full chunk
+  static_assert(CH_F4 * 4 <= kChunkFloats, "chunk must fit one LDS buffer");
   constexpr int PER_WAVE = (CH_F4 + 3) / 4;          // float4 each wave stages per chunk
   constexpr int PER_LANE = (PER_WAVE + 63) / 64;
-  constexpr int TOT_F4 = K4 * NQ * 64;               // float4 in the whole layer
   const f32x4* g4 = reinterpret_cast<const f32x4*>(wp);
   f32x4* l4 = reinterpret_cast<f32x4*>(lds);
-  f32x4 acc[NT];
+  const int g = lane >> 4;
+  // chunk element e (= (u * NQP + qq) * 64 + l) of chunk c of pass p -> packed float4 index
+  auto gidx = [&](int p, int c, int e) {
+    const int u = e / (NQP * 64), rest = e - u * (NQP * 64);
+    return ((c * kCK + u) * NQ + p * NQP) * 64 + rest;
+  };
+  auto in_layer = [&](int c, int e) { return c * kCK + e / (NQP * 64) < K4; };
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  f32x4 stage[PER_LANE];
-  // chunk 0 -> buffer 0
+  for (int p = 0; p < OS; ++p) {
+    f32x4 acc[NTP];
 #pragma unroll
-  for (int j = 0; j < PER_LANE; ++j) {
-    const int e = wave * PER_WAVE + j * 64 + lane;
-    if (e < (wave + 1) * PER_WAVE && e < CH_F4 && e < TOT_F4) l4[e] = g4[e];
-  }
-  __syncthreads();
+    for (int nt = 0; nt < NTP; ++nt) acc[nt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    f32x4 stage[PER_LANE];
+    // chunk 0 -> buffer 0
 #pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int buf = c & 1;
-    // stage chunk c+1 (L2 -> registers) while chunk c computes
-    if (c + 1 < NCH) {
-#pragma unroll
-      for (int j = 0; j < PER_LANE; ++j) {
-        const int e = wave * PER_WAVE + j * 64 + lane;
-        const int ge = (c + 1) * CH_F4 + e;
-        if (e < (wave + 1) * PER_WAVE && e < CH_F4 && ge < TOT_F4) stage[j] = g4[ge];
-      }
-    }
-    const f32x4* cur = l4 + buf * (kChunkFloats / 4);
-#pragma unroll
-    for (int u = 0; u < kCK; ++u) {
-      const int s = c * kCK + u;
-      if (s < K4) {
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const f32x4 w = cur[(u * NQ + q) * 64 + lane];
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc)
-            acc[4 * q + cc] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[cc], hin[s], acc[4 * q + cc], 0, 0, 0);
-        }
-      }
-    }
-    if (c + 1 < NCH) {
-      f32x4* nxt = l4 + (buf ^ 1) * (kChunkFloats / 4);
-#pragma unroll
-      for (int j = 0; j < PER_LANE; ++j) {
-        const int e = wave * PER_WAVE + j * 64 + lane;
-        const int ge = (c + 1) * CH_F4 + e;
-        if (e < (wave + 1) * PER_WAVE && e < CH_F4 && ge < TOT_F4) nxt[e] = stage[j];
-      }
+    for (int j = 0; j < PER_LANE; ++j) {
+      const int e = wave * PER_WAVE + j * 64 + lane;
+      if (e < (wave + 1) * PER_WAVE && e < CH_F4 && in_layer(0, e)) l4[e] = g4[gidx(p, 0, e)];
     }
     __syncthreads();
-  }
-  const int g = lane >> 4;
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
+    for (int c = 0; c < NCH; ++c) {
+      const int buf = c & 1;
+      // stage chunk c+1 (L2 -> registers) while chunk c computes
+      if (c + 1 < NCH) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) hout[4 * nt + r] = fast_tanh(acc[nt][r] + bb[r]);
+        for (int j = 0; j < PER_LANE; ++j) {
+          const int e = wave * PER_WAVE + j * 64 + lane;
+          if (e < (wave + 1) * PER_WAVE && e < CH_F4 && in_layer(c + 1, e)) stage[j] = g4[gidx(p, c + 1, e)];
+        }
+      }
+      const f32x4* cur = l4 + buf * (kChunkFloats / 4);
+      // the weights of k-step u + 1 are read from LDS while k-step u's MFMAs run (two register
+      // sets), so the LDS latency hides behind NQP x 4 MFMAs instead of stalling every group
+      f32x4 wk[NQP], wn[NQP];
+#pragma unroll
+      for (int q = 0; q < NQP; ++q) wk[q] = cur[q * 64 + lane];
+#pragma unroll
+      for (int u = 0; u < kCK; ++u) {
+        const int s = c * kCK + u;
+        if (s < K4) {
+          if (u + 1 < kCK && s + 1 < K4) {
+#pragma unroll
+            for (int q = 0; q < NQP; ++q) wn[q] = cur[((u + 1) * NQP + q) * 64 + lane];
+          }
+          // keep those LDS reads ahead of this k-step's MFMAs (the scheduler would sink them to
+          // their use); VALU / SALU / transcendental / global-memory work may still move across
+          __builtin_amdgcn_sched_barrier(0x416);
+#pragma unroll
+          for (int q = 0; q < NQP; ++q)
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc)
+              acc[4 * q + cc] = __builtin_amdgcn_mfma_f32_16x16x4f32(wk[q][cc], hin[s], acc[4 * q + cc], 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < NQP; ++q) wk[q] = wn[q];
+        }
+      }
+      if (c + 1 < NCH) {
+        f32x4* nxt = l4 + (buf ^ 1) * (kChunkFloats / 4);
+#pragma unroll
+        for (int j = 0; j < PER_LANE; ++j) {
+          const int e = wave * PER_WAVE + j * 64 + lane;
+          if (e < (wave + 1) * PER_WAVE && e < CH_F4 && in_layer(c + 1, e)) nxt[e] = stage[j];
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int nt = 0; nt < NTP; ++nt) {
+      const int tile = p * NTP + nt;
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + 16 * tile + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hout[4 * tile + r] = fast_tanh(acc[nt][r] + bb[r]);
+    }
   }
 }
 
@@ -182,10 +213,10 @@ __device__ __forceinline__ void mlp(const float* __restrict__ packed, const floa
                                     int lane, float* lds, int wave) {
   const float* bias = packed + off_b(NOUT);
   float h1[64], h2[128], h3[128], h4[64];
-  mfma_layer<13, 16>(packed + off_w1(), bias, x, h1, lane, lds, wave);
-  mfma_layer<64, 32>(packed + off_w2(), bias + kH1, h1, h2, lane, lds, wave);
-  mfma_layer<128, 32>(packed + off_w3(), bias + kH1 + kH2, h2, h3, lane, lds, wave);
-  mfma_layer<128, 16>(packed + off_w4(), bias + kH1 + kH2 + kH3, h3, h4, lane, lds, wave);
+  mfma_layer<13, 16, 1>(packed + off_w1(), bias, x, h1, lane, lds, wave);
+  mfma_layer<64, 32, kOS512>(packed + off_w2(), bias + kH1, h1, h2, lane, lds, wave);
+  mfma_layer<128, 32, kOS512>(packed + off_w3(), bias + kH1 + kH2, h2, h3, lane, lds, wave);
+  mfma_layer<128, 16, 1>(packed + off_w4(), bias + kH1 + kH2 + kH3, h3, h4, lane, lds, wave);
   const int g = lane >> 4;
 #pragma unroll
   for (int a = 0; a < NOUT; ++a) {

@@ -33,7 +33,8 @@ def random_ou(prev: torch.Tensor) -> torch.Tensor:
 
 
 def _local_device() -> str:
-    return f"cuda:{int(os.environ.get('LOCAL_RANK', 0))}"
+    # one process per GPU: LOCAL_RANK; VSS_LOCAL_DEVICE pins it (several ranks on one GPU)
+    return f"cuda:{int(os.environ.get('VSS_LOCAL_DEVICE', os.environ.get('LOCAL_RANK', 0)))}"
 
 
 def make_env(args):

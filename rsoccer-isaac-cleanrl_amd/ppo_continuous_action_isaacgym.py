@@ -291,16 +291,23 @@ def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_adv
 
 
 def setup_distributed():
+    """One process per GPU (torch.distributed.run env). RCCL ("nccl") on GPUs, gloo on CPU.
+    Rehearsal overrides (several ranks on one GPU): VSS_LOCAL_DEVICE pins the device index,
+    VSS_DIST_BACKEND=gloo picks gloo (RCCL refuses two ranks on one device)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local_device_index()
     if world > 1 and not dist.is_initialized():
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = os.environ.get("VSS_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         kw = {"device_id": torch.device(f"cuda:{local}")} if backend == "nccl" else {}
         dist.init_process_group(backend, **kw)
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
     return world, rank, local
+
+
+def local_device_index() -> int:
+    return int(os.environ.get("VSS_LOCAL_DEVICE", os.environ.get("LOCAL_RANK", "0")))
 
 
 def train(args):

@@ -243,3 +243,32 @@ def test_first_done_stats_matches_reference_loop(done_idx):
             want = [1.0] + [float(info["r"][k][idx]) for k in P.EP_KEYS] + [float(info["l"][idx])]
             break
     assert got.tolist() == pytest.approx(want) if done_idx else got[0] == 0
+
+
+@pytest.mark.gpu
+def test_train_two_ranks_gradient_allreduce_gpu(tmp_path):
+    """The data-parallel PPO loop as torch.distributed.run launches it, 2 ranks (sharing the one
+    GPU, gloo for the gradient all-reduce of device tensors): both ranks train to completion and
+    end with identical weights (one all-reduce per minibatch keeps the replicas in sync)."""
+    import subprocess
+    import sys
+    script = os.path.join(os.path.dirname(P.__file__), "ppo_continuous_action_isaacgym.py")
+    probe = os.path.join(tmp_path, "probe.py")
+    with open(probe, "w") as f:
+        f.write(
+            "import os, sys, torch\n"
+            f"sys.path.insert(0, {os.path.dirname(script)!r})\n"
+            "import ppo_continuous_action_isaacgym as P\n"
+            f"a = P.parse_args(['--env-id', 'sa', '--num-envs', '2048', '--num-steps', '16', '--update-epochs', '2',"
+            f" '--num-updates', '2', '--save-path', {str(tmp_path)!r}])\n"
+            "agent, hist = P.train(a)\n"
+            "flat = torch.cat([p.detach().reshape(-1) for p in agent.parameters()]).cpu()\n"
+            f"torch.save(flat, os.path.join({str(tmp_path)!r}, 'w%s.pt' % os.environ['RANK']))\n")
+    env = dict(os.environ, VSS_LOCAL_DEVICE="0", VSS_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), probe],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    w0 = torch.load(os.path.join(tmp_path, "w0.pt"), weights_only=True)
+    w1 = torch.load(os.path.join(tmp_path, "w1.pt"), weights_only=True)
+    assert torch.equal(w0, w1)

@@ -8,6 +8,8 @@ import pytest
 
 from vss_amd import _native as N
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 def declared_functions():
     src = open(N.HEADER).read()
@@ -74,3 +76,19 @@ def test_oracle_under_asan_ubsan():
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "oracle selftest ok" in r.stdout
+
+
+def test_c_host_demo_compiles_and_links(tmp_path):
+    """examples/vss_host_demo.c — the C ABI from plain C (hipMalloc'd buffers, no Python) —
+    compiles against include/vss.h and links against the built library (run: tests/test_c_host.py)."""
+    import shutil
+    import subprocess
+    if not shutil.which("gcc") or not os.path.exists("/opt/rocm/include/hip/hip_runtime_api.h"):
+        pytest.skip("gcc or the HIP headers are not available")
+    if not os.path.exists(N.LIB_PATH):
+        from vss_amd import build
+        build()
+    out = os.path.join(tmp_path, "vss_host_demo")
+    r = subprocess.run(["make", "-s", "-C", os.path.join(REPO, "examples"), f"OUT={out}"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert os.path.exists(out)

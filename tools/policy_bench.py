@@ -52,7 +52,7 @@ def main():
     t_fused = timeit(fused_step)
     t_ac = timeit(lambda: fused.get_action_and_value(obs))
     flop_ac = 2 * rows * (52 * 256 + 256 * 512 + 512 * 512 + 512 * 256 + 256 * 2 + 52 * 256 + 256 * 512 + 512 * 512 + 512 * 256 + 256)
-    # prefetch-depth variants built by `make OUT=tools/_build/libpol_dN.so POLICY_PREFETCH=N`
+    # build variants placed in tools/_build/libpol_*.so (e.g. hipcc ... -DVPOL_CK=.. -DVPOL_OS=.. -shared)
     import ctypes
     import glob
     from vss_amd import _native as N

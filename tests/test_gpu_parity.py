@@ -99,6 +99,39 @@ def test_full_step_free_running_bit_exact(n, steps, max_len):
     assert resets > 0 and goals > 0 and timeouts > 0
 
 
+@pytest.mark.parametrize("weights,clip", [((1.0, 0.0, 0.0, 0.0), 1.0),     # play.py's evaluation weights
+                                          ((10.0, 2.0, 3.0, 0.5), 1.0),    # energy term on
+                                          ((0.0, 0.0, 0.0, 0.0), 0.5),     # every term off, tighter clip
+                                          ((10.0, 2.0, 3.0, 0.0), float("inf"))])  # no clip
+def test_full_step_parameter_variants_bit_exact(weights, clip):
+    """The reward-weight branches (a term is skipped when its weight is 0, envs/vss.py:240-258)
+    and the VecTask action clamp, at parameters the other tests do not use; actions reach
+    +-1.6 so the clamp is exercised."""
+    n, steps = 257, 60
+    env = make_vss(n, max_len=40, seed=77, weights=weights)
+    env.clip_actions = clip
+    h = host_from(env)
+    prm = oracle_params(env)
+    gen = np.random.default_rng(5)
+    for t in range(steps):
+        a = gen.uniform(-1.6, 1.6, (n, 2, 3, 2)).astype(np.float32)
+        obs_dict, rew, reset, extras = env.step(torch.from_numpy(a).to(DEV))
+        io = O.make_io(n, O.MODE_FULL)
+        O.step(h, O.MODE_FULL, a.reshape(n, 12), io, prm)
+        msg = f"step {t}"
+        assert_env_equal(env, h, msg)
+        np.testing.assert_array_equal(bits(obs_dict["obs"]).reshape(n, 312), io["obs"].view(np.uint32).reshape(n, 312), err_msg=msg)
+        np.testing.assert_array_equal(bits(rew).reshape(n, 24), io["rew"].view(np.uint32), err_msg=msg)
+    r = rew.cpu().numpy().reshape(n, 2, 3, 4)
+    for c, w in enumerate(weights):
+        if w == 0.0:
+            assert np.all(r[..., c] == 0.0), c
+    if weights[3] > 0:
+        assert np.all(r[..., 3] <= 0.0) and np.any(r[..., 3] < 0.0)  # -mean|a| x w_energy
+    d = env.dof_velocity_buf.cpu().numpy()
+    assert np.all(np.abs(d) <= min(clip, 1.6) + 1e-7)
+
+
 @pytest.mark.parametrize("mode", [O.MODE_SA, O.MODE_CMA, O.MODE_DMA])
 @pytest.mark.parametrize("n", [4096, 67])
 def test_wrapped_step_free_running_bit_exact(mode, n):

@@ -210,6 +210,18 @@ int vss_value_forward_masked(void* stream, int64_t rows, int32_t n_act, const fl
                              float* logprob_out, float* entropy_out, float* value_out, float* mean_out,
                              const int64_t* row_mask);
 
+/* ---------------------------------------------------------------------------------------------
+ * Episode statistics: RecordEpisodeStatisticsTorch.step (envs/wrappers.py:66-87)
+ * for `rows` learner rows in one launch, in the reference's order:
+ *   ep_returns += rews; ep_lengths += 1; returned_returns = ep_returns; returned_lengths =
+ *   ep_lengths; return_sum = ((r0 + r1) + r2) + r3 of returned_returns; then
+ *   ep_returns *= 1 - dones; ep_lengths *= 1 - dones.
+ * rews, ep_returns, returned_returns: (rows, 4) fp32, 16-B aligned; ep_lengths,
+ * returned_lengths: (rows,) int32; dones: (rows,) int64; return_sum: (rows,) fp32.
+ * ------------------------------------------------------------------------------------------- */
+int vss_episode_stats(void* stream, int64_t rows, const float* rews, const int64_t* dones, float* ep_returns,
+                      int32_t* ep_lengths, float* returned_returns, int32_t* returned_lengths, float* return_sum);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1086,6 +1086,27 @@ __global__ __launch_bounds__(kWave) void observe_kernel(int64_t n, vss_state s, 
   coop_store_obs<A>(obs + f0 * (52 * A), nv, lds, lane);
 }
 
+// RecordEpisodeStatisticsTorch.step (envs/wrappers.py:66-87), one row per lane.  The products
+// by (1 - done) keep torch's float semantics: x * 0 = -0 for negative x.
+__global__ __launch_bounds__(256) void episode_stats_kernel(int64_t rows, const float4* __restrict__ rews,
+                                                            const int64_t* __restrict__ dones, float4* ep_ret,
+                                                            int32_t* ep_len, float4* __restrict__ ret_out,
+                                                            int32_t* __restrict__ len_out, float* __restrict__ sum_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows) return;
+  const float4 r = rews[i];
+  float4 e = ep_ret[i];
+  e.x = e.x + r.x; e.y = e.y + r.y; e.z = e.z + r.z; e.w = e.w + r.w;
+  const int32_t l = ep_len[i] + 1;
+  ret_out[i] = e;
+  len_out[i] = l;
+  sum_out[i] = ((e.x + e.y) + e.z) + e.w;
+  const int64_t keep = 1 - dones[i];
+  const float kf = (float)keep;
+  ep_ret[i] = make_float4(e.x * kf, e.y * kf, e.z * kf, e.w * kf);
+  ep_len[i] = (int32_t)(l * keep);
+}
+
 }  // namespace vss
 
 // ================================================================================================
@@ -1186,6 +1207,19 @@ int vss_compute_observations(void* stream, int64_t n, const vss_state* st, float
   if (n_agents == 6) hipLaunchKernelGGL(vss::observe_kernel<6>, grid, block, 0, s, n, *st, obs);
   else if (n_agents == 3) hipLaunchKernelGGL(vss::observe_kernel<3>, grid, block, 0, s, n, *st, obs);
   else hipLaunchKernelGGL(vss::observe_kernel<1>, grid, block, 0, s, n, *st, obs);
+  return launch_status();
+}
+
+int vss_episode_stats(void* stream, int64_t rows, const float* rews, const int64_t* dones, float* ep_returns,
+                      int32_t* ep_lengths, float* returned_returns, int32_t* returned_lengths, float* return_sum) {
+  if (rows < 0 || rows > (int64_t(1) << 31) || bad(rews, 16) || bad(dones, 8) || bad(ep_returns, 16) ||
+      bad(ep_lengths, 4) || bad(returned_returns, 16) || bad(returned_lengths, 4) || bad(return_sum, 4))
+    return VSS_E_ARG;
+  if (rows == 0) return VSS_OK;
+  const dim3 grid((unsigned)((rows + 255) / 256)), block(256);
+  hipLaunchKernelGGL(vss::episode_stats_kernel, grid, block, 0, (hipStream_t)stream, rows,
+                     reinterpret_cast<const float4*>(rews), dones, reinterpret_cast<float4*>(ep_returns), ep_lengths,
+                     reinterpret_cast<float4*>(returned_returns), returned_lengths, return_sum);
   return launch_status();
 }
 

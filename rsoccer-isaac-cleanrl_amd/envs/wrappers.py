@@ -55,12 +55,13 @@ def make_env(args):
 
 
 class RecordEpisodeStatisticsTorch(Wrapper):
-    """Running per-env returns (goal, grad, move, energy) and lengths (envs/wrappers.py:50-87)."""
+    """Running per-env returns (goal, grad, move, energy) and lengths (envs/wrappers.py:50-87),
+    updated by one HIP launch per step (`vss_episode_stats`) instead of seven elementwise ops."""
 
     def __init__(self, env, device):
         super().__init__(env)
         self.num_envs = getattr(env, "num_envs", 1)
-        self.device = device
+        self.device = N.require_device(device)
         self.episode_returns = None
         self.episode_lengths = None
 
@@ -71,20 +72,23 @@ class RecordEpisodeStatisticsTorch(Wrapper):
         self.episode_lengths = torch.zeros(n, dtype=torch.int32, device=self.device)
         self.returned_episode_returns = torch.zeros_like(self.episode_returns)
         self.returned_episode_lengths = torch.zeros_like(self.episode_lengths)
+        self.returned_return_sum = torch.zeros(n, dtype=torch.float32, device=self.device)
         return observations
 
     def step(self, action):
         observations, rewards, dones, infos = super().step(action)
-        self.episode_returns += infos["rews"]
-        self.episode_lengths += 1
-        self.returned_episode_returns.copy_(self.episode_returns)
-        self.returned_episode_lengths.copy_(self.episode_lengths)
-        keep = 1 - dones
-        self.episode_returns *= keep.unsqueeze(1)
-        self.episode_lengths *= keep.to(self.episode_lengths.dtype)
+        rews = infos["rews"]
+        n = self.num_envs
+        if (rews.shape != (n, 4) or rews.dtype != torch.float32 or not rews.is_contiguous()
+                or dones.numel() != n or dones.dtype != torch.long or not dones.is_contiguous()):
+            raise ValueError("episode statistics expect rews (N, 4) float32 and dones (N,) int64, contiguous")
+        N.check(N.load().vss_episode_stats(
+            N.stream_of(self.device), n, rews.data_ptr(), dones.data_ptr(), self.episode_returns.data_ptr(),
+            self.episode_lengths.data_ptr(), self.returned_episode_returns.data_ptr(),
+            self.returned_episode_lengths.data_ptr(), self.returned_return_sum.data_ptr()), "vss_episode_stats")
         r = self.returned_episode_returns
         infos["r"] = {"goal": r[:, 0], "grad": r[:, 1], "move": r[:, 2], "energy": r[:, 3],
-                      "return": r.sum(1)}
+                      "return": self.returned_return_sum}
         infos["l"] = self.returned_episode_lengths
         return observations, rewards, dones, infos
 

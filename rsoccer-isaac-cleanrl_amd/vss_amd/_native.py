@@ -25,7 +25,7 @@ CH_BALL_X, CH_BALL_Y, CH_BALL_VX, CH_BALL_VY = 0, 1, 2, 3
 CH_RX, CH_RY, CH_RQX, CH_RQY, CH_RQZ, CH_RQW, CH_RVX, CH_RVY, CH_RW = 4, 10, 16, 22, 28, 34, 40, 46, 52
 EXPORTED = ("vss_abi_version", "vss_error_string", "vss_step", "vss_rollout", "vss_reset_dones",
             "vss_compute_observations", "vss_mlp_packed_size", "vss_mlp_pack", "vss_policy_forward",
-            "vss_value_forward_masked")
+            "vss_value_forward_masked", "vss_episode_stats")
 
 
 class VssParams(ctypes.Structure):
@@ -93,6 +93,8 @@ def load() -> ctypes.CDLL:
     L.vss_policy_forward.restype = ctypes.c_int
     L.vss_value_forward_masked.argtypes = [P, i64, i32, P, P, P, P, ctypes.c_uint64, ctypes.c_uint64] + [P] * 7
     L.vss_value_forward_masked.restype = ctypes.c_int
+    L.vss_episode_stats.argtypes = [P, i64] + [P] * 7
+    L.vss_episode_stats.restype = ctypes.c_int
     if L.vss_abi_version() != ABI_VERSION:
         raise NativeError(f"libvss_amd ABI {L.vss_abi_version()} != expected {ABI_VERSION}")
     _lib = L

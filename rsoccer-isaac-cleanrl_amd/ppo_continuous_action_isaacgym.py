@@ -132,6 +132,55 @@ class Agent(nn.Module):
         return action, probs.log_prob(action).sum(1), probs.entropy().sum(1), self.critic(x)
 
 
+# ---- the update's Linear layers with a split-K weight gradient ------------------------------------
+# dW = dY^T X reduces over all minibatch rows (2,097,152 at 65,536 envs) into a small output
+# (<= 512 x 512); as one GEMM hipBLASLt runs the 256<->512, first and last layers of the Agent at
+# 0.6-72 TF.  Splitting the rows into SPLITK chunks (one batched GEMM + a sum) runs them at
+# ~150 TF (tools/wgrad_bench.py): -0.9 s per update.  Forward and input gradient are unchanged
+# (addmm with bias = what nn.Linear issues; dY W); only the fp32 summation order of dW differs.
+SPLITK = 64
+SPLITK_MIN_ROWS = 65536
+
+
+class _LinearSplitK(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        return torch.addmm(bias, x, weight.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gx = gy.mm(weight) if ctx.needs_input_grad[0] else None
+        rows = x.shape[0]
+        if rows >= SPLITK_MIN_ROWS and rows % SPLITK == 0:
+            gw = torch.bmm(gy.reshape(SPLITK, rows // SPLITK, gy.shape[1]).transpose(1, 2),
+                           x.reshape(SPLITK, rows // SPLITK, x.shape[1])).sum(0)
+        else:
+            gw = gy.t().mm(x)
+        return gx, gw, gy.sum(0)
+
+
+def _mlp_forward(seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+    for m in seq:
+        if isinstance(m, nn.Linear):
+            x = _LinearSplitK.apply(x, m.weight, m.bias)
+        elif isinstance(m, nn.Tanh):
+            x = torch.tanh(x)
+        else:
+            x = m(x)
+    return x
+
+
+def get_action_and_value_update(agent: "Agent", x, action):
+    """Agent.get_action_and_value (ppo…:157-164) on the same parameters, for the PPO update:
+    identical forward, split-K weight gradients in the backward."""
+    mean = _mlp_forward(agent.actor_mean, x)
+    std = torch.exp(agent.actor_logstd.expand_as(mean))
+    probs = Normal(mean, std)
+    return action, probs.log_prob(action).sum(1), probs.entropy().sum(1), _mlp_forward(agent.critic, x)
+
+
 class ExtractObsWrapper(ObservationWrapper):
     def observation(self, obs):
         return obs["obs"]
@@ -242,8 +291,11 @@ def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_adv
         b_inds = torch.randperm(batch, device=device, generator=gen)
         for start in range(0, batch, mb):
             mb_inds = b_inds[start:start + mb]
-            with autocast(args, device):
-                _, newlogprob, entropy, newvalue = agent.get_action_and_value(b_obs[mb_inds], b_actions[mb_inds])
+            if getattr(args, "amp", "none") == "none":
+                _, newlogprob, entropy, newvalue = get_action_and_value_update(agent, b_obs[mb_inds], b_actions[mb_inds])
+            else:
+                with autocast(args, device):
+                    _, newlogprob, entropy, newvalue = agent.get_action_and_value(b_obs[mb_inds], b_actions[mb_inds])
             newlogprob, entropy, newvalue = newlogprob.float(), entropy.float(), newvalue.float()
             logratio = newlogprob - b_logprobs[mb_inds]
             ratio = logratio.exp()

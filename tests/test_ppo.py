@@ -272,3 +272,23 @@ def test_train_two_ranks_gradient_allreduce_gpu(tmp_path):
     w0 = torch.load(os.path.join(tmp_path, "w0.pt"), weights_only=True)
     w1 = torch.load(os.path.join(tmp_path, "w1.pt"), weights_only=True)
     assert torch.equal(w0, w1)
+
+
+@pytest.mark.parametrize("rows", [256, 65536 + 64 * 3])
+def test_update_forward_and_splitk_gradients_match_autograd(rows):
+    """The update's functional forward equals Agent.get_action_and_value, and the split-K weight
+    gradients equal autograd's (fp32 summation order only)."""
+    agent = make_agent(2)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(rows, 52, generator=g)
+    a = torch.randn(rows, 2, generator=g) * 0.5
+    outs_ref = agent.get_action_and_value(x, a)
+    loss_ref = outs_ref[1].sum() + outs_ref[2].sum() + outs_ref[3].sum()
+    grads_ref = torch.autograd.grad(loss_ref, list(agent.parameters()))
+    outs = P.get_action_and_value_update(agent, x, a)
+    for u, v in zip(outs[1:], outs_ref[1:]):
+        torch.testing.assert_close(u, v, rtol=0, atol=0)   # same forward ops
+    loss = outs[1].sum() + outs[2].sum() + outs[3].sum()
+    grads = torch.autograd.grad(loss, list(agent.parameters()))
+    for (name, _), u, v in zip(agent.named_parameters(), grads, grads_ref):
+        torch.testing.assert_close(u, v, rtol=2e-4, atol=2e-4 * float(v.abs().max()) + 1e-6, msg=name)

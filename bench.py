@@ -12,8 +12,9 @@ and the max-over-ranks of the elapsed time.
 
 Rank 0 prints ONE JSON line (value = env-steps/s summed over all ranks = fields x ranks x K /
 max-over-ranks time).  `roofline.achieved` = algorithmic bytes per launch / mean launch time
-measured with HIP events on the launch stream; `cpu_baseline` = the C oracle (oracle/) on one
-host core over a bounded sample.
+measured with HIP events on the launch stream; `cpu_baseline` = the C oracle (oracle/, the only
+use of it here) on the host's cores (one 4,096-field shard per thread, up to 16) over a bounded
+sample, with its one-thread rate beside it.
 """
 from __future__ import annotations
 

@@ -85,6 +85,9 @@ def parse_args(argv=None):
     p.add_argument("--fused-policy", type=b, default=True, nargs="?", const=True,
                    help="rollout forward with the fused HIP MLP kernel (vss_policy_forward); "
                         "terminal values only for the fields that reset")
+    p.add_argument("--evaluate", type=b, default=False, nargs="?", const=True,
+                   help="after training, play matches vs the baseline teams (ppo…:380-461, no W&B)")
+    p.add_argument("--eval-matches", type=int, default=10000, help="matches per baseline team")
     p.add_argument("--amp", type=str, default="none", choices=["none", "bf16"],
                    help="bf16 autocast for the MLP GEMMs (off = the reference's fp32 numerics)")
     args = p.parse_args(argv)
@@ -358,6 +361,41 @@ def setup_distributed():
     return world, rank, local
 
 
+def evaluate(args, unwrapped_env, checkpoint: str, writer, global_step: int) -> dict:
+    """Post-training evaluation (ppo…:380-461) without W&B: goal-only rewards, the trained agent
+    as the blue team against every baseline team available (play.py: zero, OU and the
+    base_nets checkpoints present), `args.eval_matches` matches each; for SA also as 'sa-x3'
+    (the single-agent policy controlling all three blue robots).  Scores go to the writer under
+    the reference's Validation/* names and are returned."""
+    from play import baseline_teams, get_team, play_matches
+    unwrapped_env.w_goal, unwrapped_env.w_grad, unwrapped_env.w_move, unwrapped_env.w_energy = 1.0, 0.0, 0.0, 0.0
+    device = unwrapped_env.device
+    teams = baseline_teams(device=str(device))
+    variants = [f"ppo-{args.env_id}"] + (["ppo-sa-x3"] if args.env_id == "sa" else [])
+    out = {}
+    for algo in variants:
+        blue = get_team(algo, checkpoint, str(device))
+        scores, lengths = [], []
+        res = {}
+        for team, seeds in teams.items():
+            t_score = t_len = 0.0
+            for seed, yellow in seeds.items():
+                r, ln = play_matches(unwrapped_env, blue, yellow, args.eval_matches)
+                t_score += r
+                t_len += ln
+                scores.append(r)
+                lengths.append(ln)
+            res[f"Validation/Score/{team}"] = t_score / len(seeds)
+            res[f"Validation/Length/{team}"] = t_len / len(seeds)
+        res["Validation/Score Mean"] = sum(scores) / len(scores)
+        res["Validation/Length Mean"] = sum(lengths) / len(lengths)
+        for k, v in res.items():
+            writer.add_scalar(f"{algo}/{k}", v, global_step)
+        print(f"evaluation {algo}: " + ", ".join(f"{k} {v:.3f}" for k, v in res.items()), flush=True)
+        out[algo] = res
+    return out
+
+
 def local_device_index() -> int:
     return int(os.environ.get("VSS_LOCAL_DEVICE", os.environ.get("LOCAL_RANK", "0")))
 
@@ -490,10 +528,13 @@ def train(args):
     if rank == 0 and args.log:
         os.makedirs(f"{args.save_path}/{run_name}", exist_ok=True)
         torch.save(agent.state_dict(), f"{args.save_path}/{run_name}/{run_name}-agent.pt")
+        wall = time.time() - start_time
+        if args.evaluate:
+            history.append({"validation": evaluate(args, unwrapped_env, f"{args.save_path}/{run_name}/{run_name}-agent.pt",
+                                                   writer, global_step)})
         # the loss / SPS curves (what the reference sends to TensorBoard/W&B), one record per update
         with open(f"{args.save_path}/{run_name}/history.json", "w") as f:
-            json.dump({"args": vars(args), "world": world, "wall_s": time.time() - start_time,
-                       "history": history}, f, indent=1)
+            json.dump({"args": vars(args), "world": world, "wall_s": wall, "history": history}, f, indent=1)
     writer.close()
     return agent, history
 

@@ -292,3 +292,18 @@ def test_update_forward_and_splitk_gradients_match_autograd(rows):
     grads = torch.autograd.grad(loss, list(agent.parameters()))
     for (name, _), u, v in zip(agent.named_parameters(), grads, grads_ref):
         torch.testing.assert_close(u, v, rtol=2e-4, atol=2e-4 * float(v.abs().max()) + 1e-6, msg=name)
+
+
+@pytest.mark.gpu
+def test_post_training_evaluation_gpu(tmp_path):
+    """--evaluate (ppo…:380-461 without W&B): the trained SA agent, and the same policy on all
+    three blue robots (sa-x3), play the baseline teams present (zero, OU); scores in [-1, 1]."""
+    args = P.parse_args(["--env-id", "sa", "--num-envs", "2048", "--num-steps", "16", "--update-epochs", "1",
+                         "--num-updates", "1", "--save-path", str(tmp_path), "--evaluate", "--eval-matches", "64"])
+    _, hist = P.train(args)
+    val = hist[-1]["validation"]
+    assert set(val) == {"ppo-sa", "ppo-sa-x3"}
+    for res in val.values():
+        assert {"Validation/Score/zero", "Validation/Score/ou", "Validation/Score Mean", "Validation/Length Mean"} <= set(res)
+        assert all(-1.0 <= res[k] <= 1.0 for k in res if "Score" in k)
+        assert res["Validation/Length Mean"] > 0

@@ -152,6 +152,36 @@ def rollout_leg(env, K: int, steps: int, gen, dev) -> dict:
                          "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": algo, "kernel_ms": launch_ms}}
 
 
+def sa_leg(env, steps: int, gen, dev) -> dict:
+    """The SA contract (SingleAgent fused into the step: what ppo-sa drives) on the same fields,
+    after the FULL measurement: `steps` launches timed with HIP events on the launch stream."""
+    from envs import wrappers as Wr
+    from vss_amd import _native as N
+    n = env.num_fields
+    W = Wr.SingleAgent(env)
+    pool = [torch.rand((n, 2), device=dev, generator=gen) * 2 - 1 for _ in range(16)]
+    io = dict(ou_buf=W.action_buf, obs=W._obs, terminal_obs=W._terminal_obs, rew=W._rews,
+              reward_sum=W._reward, dones_rep=None, time_outs=W._time_outs, progress_f=W._progress)
+    for k in range(20):
+        env.native_step(N.MODE_SA, pool[k % 16], io)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for k in range(steps):
+        env.native_step(N.MODE_SA, pool[k % 16], io)
+    e1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1) / steps
+    algo = BYTES["sa"] * n
+    achieved = algo / (ms * 1e-3)
+    return {"value": n * steps / wall, "unit": "env-steps/s", "steps": steps, "ms_per_step": ms,
+            "note": "wall time includes the Python wrapper's per-call buffer checks; kernel time is ms_per_step",
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": algo, "kernel_ms": ms}}
+
+
 def ppo_wallclock(n_envs: int, updates: int, dev) -> dict:
     """The full SA PPO loop (ppo_continuous_action_isaacgym.py, reference defaults: T=128,
     8 epochs x 4 minibatches, fp32) at `n_envs` envs; the last update is timed and projected to
@@ -342,6 +372,8 @@ def main():
         }
         if args.rollout_k > 0 and mode == N.MODE_FULL:
             out["rollout"] = rollout_leg(env, args.rollout_k, args.steps, gen, dev)
+        if mode == N.MODE_FULL:
+            out["sa_step"] = sa_leg(env, args.steps, gen, dev)
         ppo_updates = args.ppo_updates if args.ppo_updates is not None else (2 if world == 1 else 0)
         if ppo_updates > 0:
             out["ppo"] = ppo_wallclock(n, ppo_updates, dev)

@@ -305,7 +305,11 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # HIP events over the timed region, on the launch stream (torch's current stream, which the
+    # ctypes launches use): average launch duration = region / K, back to back
+    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    r0.record()
     if graph is not None:
         for _ in range(args.steps // len(cios)):
             graph.replay()
@@ -314,13 +318,15 @@ def main():
     else:
         for k in range(args.steps):
             launch(k)
+    r1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    region_ms = r0.elapsed_time(r1) / args.steps
 
-    # ---- kernel duration: per-launch HIP events on the launch stream (torch's current
-    # stream), a separate pass of the same launches so the events do not perturb the timing ----
+    # ---- diagnostic: per-launch HIP events (a separate pass of the same launches; each event
+    # pair adds its own overhead, so this reads ~2-3 % above the region average) ----
     n_ev = min(args.steps, 100)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
     for k in range(n_ev):
@@ -328,9 +334,10 @@ def main():
         launch(k)
         ev[k][1].record()
     torch.cuda.synchronize()
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    per_launch_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
-    elapsed, kern_ms = reduce_max([elapsed, kern_ms], dev if args.dist_backend == "nccl" else "cpu")
+    elapsed, kern_ms, per_launch_ms = reduce_max([elapsed, region_ms, per_launch_ms],
+                                                 dev if args.dist_backend == "nccl" else "cpu")
 
     if rank == 0:
         agents = 3 if args.mode == "dma" else 1
@@ -368,7 +375,8 @@ def main():
                        "parallelism": f"fields sharded over {world} GPU(s), no data-path collective"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "traffic": traffic,
-                         "algorithmic_bytes_per_launch": algo, "kernel_ms": kern_ms},
+                         "algorithmic_bytes_per_launch": algo, "kernel_ms": kern_ms,
+                         "kernel_ms_per_launch_events": per_launch_ms},
         }
         if args.rollout_k > 0 and mode == N.MODE_FULL:
             out["rollout"] = rollout_leg(env, args.rollout_k, args.steps, gen, dev)

@@ -61,7 +61,7 @@ def parse():
     p.add_argument("--rollout-k", type=int, default=16,
                    help="also time vss_rollout with K steps per launch (0 = skip)")
     p.add_argument("--ppo-updates", type=int, default=None,
-                   help="PPO training updates timed after the env-step benchmark (default: 2 at N=1, 0 otherwise)")
+                   help="PPO training updates timed after the env-step benchmark, on every rank (default 2)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL) for real multi-GPU runs; gloo + --share-gpu to rehearse ranks on one GPU")
     p.add_argument("--share-gpu", action="store_true", help="map every rank to cuda:0 (rehearsal only)")
@@ -182,23 +182,31 @@ def sa_leg(env, steps: int, gen, dev) -> dict:
                          "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": algo, "kernel_ms": ms}}
 
 
-def ppo_wallclock(n_envs: int, updates: int, dev) -> dict:
+def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
     """The full SA PPO loop (ppo_continuous_action_isaacgym.py, reference defaults: T=128,
-    8 epochs x 4 minibatches, fp32) at `n_envs` envs; the last update is timed and projected to
-    1e8 env-steps (ceil(1e8 / batch) updates; the reference's floor-division gives one fewer)."""
+    8 epochs x 4 minibatches, fp32) at `n_envs` envs per rank; the last update is timed and
+    projected to 1e8 env-steps (ceil(1e8 / global batch) updates; the reference's floor-division
+    gives one fewer).  Runs on EVERY rank: at N > 1 each rank owns its own `n_envs` fields and
+    the gradients are averaged by one flat all-reduce per minibatch (RCCL), so the figures here
+    are max-over-ranks times and whole-job (all-rank) env-steps."""
     import math
     import ppo_continuous_action_isaacgym as P
     args = P.parse_args(["--env-id", "sa", "--num-envs", str(n_envs), "--num-updates", str(updates),
                          "--log", "false", "--seed", "1"])
     _, hist = P.train(args)
     last = hist[-1]
-    per_update = last["rollout_s"] + last["update_s"]
-    batch = args.batch_size
+    roll_s, upd_s = reduce_max([last["rollout_s"], last["update_s"]],
+                               dev if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu")
+    per_update = roll_s + upd_s
+    batch = args.batch_size * world
     updates_1e8 = math.ceil(1e8 / batch)
-    return {"env": "sa", "num_envs": n_envs, "num_steps": args.num_steps, "batch": batch,
-            "update_epochs": args.update_epochs, "num_minibatches": args.num_minibatches, "dtype": "f32",
-            "rollout_s": last["rollout_s"], "update_s": last["update_s"],
-            "rollout_env_steps_per_s": batch / last["rollout_s"], "train_env_steps_per_s": batch / per_update,
+    return {"env": "sa", "n_gpus": world, "num_envs": n_envs * world, "num_envs_per_gpu": n_envs,
+            "num_steps": args.num_steps, "batch": batch, "update_epochs": args.update_epochs,
+            "num_minibatches": args.num_minibatches, "dtype": "f32",
+            "gradient_exchange": ("one flat fp32 all-reduce per minibatch "
+                                  f"({dist.get_backend() if dist.is_initialized() else 'none'})") if world > 1 else "none",
+            "rollout_s": roll_s, "update_s": upd_s,
+            "rollout_env_steps_per_s": batch / roll_s, "train_env_steps_per_s": batch / per_update,
             "wallclock_to_1e8_steps_s": updates_1e8 * per_update, "updates_to_1e8": updates_1e8,
             "timed_update": len(hist)}
 
@@ -339,6 +347,17 @@ def main():
     elapsed, kern_ms, per_launch_ms = reduce_max([elapsed, region_ms, per_launch_ms],
                                                  dev if args.dist_backend == "nccl" else "cpu")
 
+    # ---- the PPO train loop on every rank (its gradient all-reduce is the one real exchange
+    # step of the path); after the env-step timing, before the rank-0-only legs ----
+    ppo = None
+    ppo_updates = args.ppo_updates if args.ppo_updates is not None else 2
+    if ppo_updates > 0:
+        if args.share_gpu:
+            os.environ["VSS_LOCAL_DEVICE"] = "0"
+        if world > 1:
+            dist.barrier()
+        ppo = ppo_wallclock(n, ppo_updates, dev, world)
+
     if rank == 0:
         agents = 3 if args.mode == "dma" else 1
         value = n * world * args.steps / elapsed
@@ -382,9 +401,8 @@ def main():
             out["rollout"] = rollout_leg(env, args.rollout_k, args.steps, gen, dev)
         if mode == N.MODE_FULL:
             out["sa_step"] = sa_leg(env, args.steps, gen, dev)
-        ppo_updates = args.ppo_updates if args.ppo_updates is not None else (2 if world == 1 else 0)
-        if ppo_updates > 0:
-            out["ppo"] = ppo_wallclock(n, ppo_updates, dev)
+        if ppo is not None:
+            out["ppo"] = ppo
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -645,7 +645,7 @@ __device__ __forceinline__ void reset_field(Bodies& b, uint32_t k0, uint32_t k1,
 #pragma unroll
       for (int j = i + 1; j < 7; ++j) {
         float dx = px[i] - px[j], dy = py[i] - py[j];
-        close |= sqrtf(dx * dx + dy * dy) < K_MIN_DIST;
+        close |= dx * dx + dy * dy < __uint_as_float(0x3ba0902du);  // == sqrtf(d2) < 0.07f (see below)
       }
     if (!close || round + 1 >= (uint32_t)kMaxRejectRounds) break;
   }
@@ -666,6 +666,66 @@ __device__ __forceinline__ void reset_field(Bodies& b, uint32_t k0, uint32_t k1,
   }
   b.bvx = u01(o[6]) - 0.5f;
   b.bvy = u01(o[7]) - 0.5f;
+}
+
+// The same reset with the field's two lane halves (L, L + 32) sharing the work: each half draws
+// two of the four position blocks and one of the two angle blocks, the values are exchanged with
+// v_permlane32_swap, and each half builds three of the six yaw quaternions.  The placement test
+// compares squared distances with kMinDist2, the smallest float whose correctly rounded sqrtf is
+// >= 0.07f, so `d2 < kMinDist2` is exactly `sqrtf(d2) < 0.07f` (what reset_field and the oracle
+// evaluate) without the square roots.  Identical values in every lane to reset_field().
+__device__ __forceinline__ void reset_field_split(Bodies& b, uint32_t k0, uint32_t k1, uint32_t field, uint32_t ctr,
+                                                  uint32_t ext) {
+  const float kMinDist2 = __uint_as_float(0x3ba0902du);  // 0.0048999996f (tests/test_oracle_golden.py)
+  const bool up = threadIdx.x >= 32;
+  const uint32_t blk0 = up ? 2u : 0u;
+  const float scale_x = 1.5f - 0.14f, scale_y = 1.3f - 0.14f;
+  float px[8], py[8];
+  for (uint32_t round = 0;; ++round) {
+    uint32_t o[8];
+    philox(k0, k1, field, ctr, ((kPurposePos | ext) << 24) | round, blk0, o);
+    philox(k0, k1, field, ctr, ((kPurposePos | ext) << 24) | round, blk0 + 1u, o + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {  // entities e (lower half) and 4 + e (upper half)
+      exch((u01(o[2 * e]) - 0.5f) * scale_x, px[e], px[4 + e]);
+      exch((u01(o[2 * e + 1]) - 0.5f) * scale_y, py[e], py[4 + e]);
+    }
+    bool close = false;
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+#pragma unroll
+      for (int j = i + 1; j < 7; ++j) {
+        float dx = px[i] - px[j], dy = py[i] - py[j];
+        close |= dx * dx + dy * dy < kMinDist2;
+      }
+    if (!close || round + 1 >= (uint32_t)kMaxRejectRounds) break;
+  }
+  b.bx = px[0]; b.by = py[0];
+  uint32_t oa[4], ang_u[8];
+  philox(k0, k1, field, ctr, ((kPurposeAng | ext) << 24), up ? 1u : 0u, oa);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float lo, hi;
+    exch(__uint_as_float(oa[i]), lo, hi);
+    ang_u[i] = __float_as_uint(lo);
+    ang_u[4 + i] = __float_as_uint(hi);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {  // robots k (lower half) and k + 3 (upper half)
+    float ang = K_TWO_PI * u01(up ? ang_u[k + 3] : ang_u[k]) + (-K_PI);
+    float sh, ch;
+    sincos_small(ang * 0.5f, sh, ch);
+    float nrm = sqrtf(sh * sh + ch * ch);
+    exch(sh / nrm, b.qz[k], b.qz[k + 3]);
+    exch(ch / nrm, b.qw[k], b.qw[k + 3]);
+  }
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    b.x[r] = px[1 + r]; b.y[r] = py[1 + r];
+    b.vx[r] = 0.0f; b.vy[r] = 0.0f; b.w[r] = 0.0f;
+  }
+  b.bvx = u01(ang_u[6]) - 0.5f;
+  b.bvy = u01(ang_u[7]) - 0.5f;
 }
 
 // ---- rewards and dones (compute_rewards_and_dones, envs/vss.py:218-265, 578-655) --------------------
@@ -828,11 +888,14 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   float dof[12];
 #pragma unroll
   for (int k = 0; k < 12; ++k) dof[k] = a[k];
+#ifndef VSS_PROF_SKIP_RESET
   if (valid && done) {
-    reset_field(b, k0, k1, (uint32_t)f, ctr, 0u);
+    if constexpr (kSplit) reset_field_split(b, k0, k1, (uint32_t)f, ctr, 0u);
+    else reset_field(b, k0, k1, (uint32_t)f, ctr, 0u);
 #pragma unroll
     for (int k = 0; k < 12; ++k) dof[k] = dof[k] * 0.0f;
   }
+#endif
 
   // -- observation after reset (envs/vss.py:203) -------------------------------------------------------------
   if (lane < kFpw) write_obs_record<A>(orec, b, dof);
@@ -1010,7 +1073,8 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
 #pragma unroll
     for (int i = 0; i < 12; ++i) dof[i] = a[i];
     if (valid && done) {
-      reset_field(b, k0, k1, (uint32_t)f, ctr + (uint32_t)k, 0u);
+      if constexpr (kSplit) reset_field_split(b, k0, k1, (uint32_t)f, ctr + (uint32_t)k, 0u);
+      else reset_field(b, k0, k1, (uint32_t)f, ctr + (uint32_t)k, 0u);
 #pragma unroll
       for (int i = 0; i < 12; ++i) dof[i] = dof[i] * 0.0f;
     }

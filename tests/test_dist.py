@@ -47,13 +47,15 @@ def test_bench_timing_is_max_over_ranks_gloo():
 def test_bench_two_ranks_rehearsal(launcher):
     """bench.py as the driver launches it for N>1 (torch.distributed.run) and as a user runs it
     by hand (`bench.py --gpus 2` starts the launcher itself), 2 ranks sharing the one GPU with
-    gloo for the barrier/timing reduce: one JSON line, value counts both ranks."""
+    gloo for the barrier/timing reduce: one JSON line, value counts both ranks; the PPO leg runs
+    on both ranks with the gradient all-reduce and reports whole-job env-steps."""
     port = _free_port()
     run = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port)] if launcher == "torchrun" else [sys.executable]
     cmd = run + [os.path.join(REPO, "bench.py"),
                  "--gpus", "2", "--steps", "20", "--warmup", "2", "--fields", "8192", "--dist-backend", "gloo",
-                 "--share-gpu", "--no-cpu-baseline"]
+                 "--share-gpu", "--no-cpu-baseline",
+                 "--ppo-updates", "1", "--rollout-k", "0"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -61,3 +63,6 @@ def test_bench_two_ranks_rehearsal(launcher):
     j = json.loads(lines[0])
     assert j["n_gpus"] == 2 and j["scaling"] == "weak" and j["value"] > 0
     assert abs(j["value"] - 2 * 8192 * 20 / (j["ms_per_step"] * 1e-3 * 20)) / j["value"] < 1e-6
+    ppo = j["ppo"]
+    assert ppo["n_gpus"] == 2 and ppo["num_envs"] == 2 * 8192 and ppo["batch"] == 2 * 8192 * 128
+    assert "all-reduce" in ppo["gradient_exchange"] and ppo["train_env_steps_per_s"] > 0

@@ -203,3 +203,18 @@ def test_wrapped_step_matches_reference(golden_dir, mode_name):
     assert g["dones"].sum() > 0
     if mode == O.MODE_DMA:
         assert int(g["num_envs"]) == 3 * n  # DMA re-assigns num_environments (envs/wrappers.py:154)
+
+
+def test_reset_placement_threshold_is_exact():
+    """The HIP reset compares squared distances with 0x3ba0902d (csrc/vss_step.hip
+    reset_field_split): the smallest float whose correctly rounded sqrt is >= 0.07f, so
+    `d2 < T` is exactly the oracle's / reference's `sqrtf(d2) < 0.07` (envs/vss.py:293-298)."""
+    c = np.float32(0.07)
+    t = np.array([0x3ba0902d], dtype=np.uint32).view(np.float32)[0]
+    below = np.nextafter(t, np.float32(0))
+    assert np.sqrt(t) >= c and np.sqrt(below) < c
+    # every float around the boundary (and a random sweep) classifies identically both ways
+    around = (t.view(np.uint32) + np.arange(-4096, 4096, dtype=np.int64)).astype(np.uint32).view(np.float32)
+    sweep = np.random.default_rng(0).uniform(0, 0.02, 200_000).astype(np.float32)
+    for d2 in (around, sweep):
+        assert np.array_equal(np.sqrt(d2) < c, d2 < t)

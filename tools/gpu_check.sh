@@ -40,6 +40,10 @@ case ",$STEPS," in *,pmc,*)
       python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
 esac
  case ",$STEPS," in *,ablate,*) run ablate 300 python tools/ablate.py ;; esac
+case ",$STEPS," in *,ablsa,*)
+  ABLATE_MODE=sa ABLATE_REPS=7 run ablate_sa 300 python tools/ablate.py
+  ABLATE_MODE=full ABLATE_REPS=7 run ablate_full 300 python tools/ablate.py ;; esac
+case ",$STEPS," in *,tdist,*) run pytest_dist 600 python -m pytest tests/test_dist.py -m gpu -x -q ;; esac
 case ",$STEPS," in *,amp,*) run ppo_amp 900 python rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 2 --amp bf16 --save-path /tmp/runs ;; esac
 case ",$STEPS," in *,ppoprof,*)
   run rocprof_ppo 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_ppo_$TAG" -o run -- \

@@ -211,6 +211,19 @@ int vss_value_forward_masked(void* stream, int64_t rows, int32_t n_act, const fl
                              const int64_t* row_mask);
 
 /* ---------------------------------------------------------------------------------------------
+ * PPO-update helper: the backward of a hidden layer's tanh
+ * (ppo_continuous_action_isaacgym.py:104-111, autograd of nn.Tanh + nn.Linear's bias) in one pass:
+ *   grad_in = grad_out * (1 - y^2)             (rows, cols) row-major, y = tanh output
+ *   bias_partial[c][j] = sum of grad_in[r][j] over the rows r of chunk c
+ * with vss_tanh_grad_chunks(rows) chunks of consecutive rows; the bias gradient is the sum of
+ * bias_partial over its chunks (caller-side, deterministic).  cols in {64, 128, 256, 512, 1024};
+ * every pointer 16-B aligned.  Replaces torch's tanh_backward + the bias-gradient reduction.
+ * ------------------------------------------------------------------------------------------- */
+int64_t vss_tanh_grad_chunks(int64_t rows);
+int vss_tanh_grad_bias(void* stream, int64_t rows, int32_t cols, const float* grad_out, const float* y,
+                       float* grad_in, float* bias_partial);
+
+/* ---------------------------------------------------------------------------------------------
  * Episode statistics: RecordEpisodeStatisticsTorch.step (envs/wrappers.py:66-87)
  * for `rows` learner rows in one launch, in the reference's order:
  *   ep_returns += rews; ep_lengths += 1; returned_returns = ep_returns; returned_lengths =

@@ -271,9 +271,17 @@ class VSS:
         N.check(rc, "vss_compute_observations")
         return out
 
-    # no viewer on this build
-    def render(self, mode="rgb_array"):
-        return None
+    def render(self, mode="rgb_array", env_id: int = 0, width: int = 400, height: int = 300):
+        """Top-down RGB frame of field `env_id` (the Isaac Gym viewer capture behind capture_video,
+        ppo…:213-221; envs/render.py); other modes (the interactive viewer) return None."""
+        if mode != "rgb_array":
+            return None
+        from .render import render_field
+        s = self.state[:, int(env_id)].detach().cpu().numpy().astype(np.float64)
+        qz, qw = s[N.CH_RQZ:N.CH_RQZ + 6], s[N.CH_RQW:N.CH_RQW + 6]
+        yaw = np.arctan2(2.0 * qw * qz, qw * qw - qz * qz)  # get_euler_xyz yaw with qx = qy = 0
+        robots = np.stack([s[N.CH_RX:N.CH_RX + 6], s[N.CH_RY:N.CH_RY + 6], yaw], 1)
+        return render_field(s[[N.CH_BALL_X, N.CH_BALL_Y]], robots, width, height)
 
     def close(self):
         pass

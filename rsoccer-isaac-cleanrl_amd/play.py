@@ -116,6 +116,10 @@ def play_matches(envs, blue_team, yellow_team, n_matches, video_path=None, chunk
     k = min(COUNT_FIELDS, n)
     action_buf = torch.zeros((n,) + tuple(envs.action_space.shape), device=envs.device)
     obs = envs.reset()["obs"]
+    rec = None
+    if video_path:  # play.py:134-142: the first 300 steps of field 0 (envs/render.py, GIF)
+        from envs.render import FrameRecorder
+        rec = FrameRecorder(lambda: envs.render("rgb_array"), video_path, lambda step: step == 0, 300, "video.000")
     ep_count, rew_sum, len_sum = 0, 0.0, 0.0
     while ep_count < n_matches:
         cnt = torch.zeros(chunk, device=envs.device, dtype=torch.int64)
@@ -125,6 +129,8 @@ def play_matches(envs, blue_team, yellow_team, n_matches, video_path=None, chunk
             blue_team(action_buf[:, 0], obs[:, 0])
             yellow_team(action_buf[:, 1], obs[:, 1])
             o, rew, dones, info = envs.step(action_buf)
+            if rec is not None:
+                rec.on_step()
             obs = o["obs"]
             d = dones[:k] != 0
             cnt[t] = d.sum()
@@ -138,4 +144,6 @@ def play_matches(envs, blue_team, yellow_team, n_matches, video_path=None, chunk
                 ep_count += int(c[t])
                 rew_sum += float(r[t])
                 len_sum += float(l[t])
+    if rec is not None:
+        rec.flush()
     return rew_sum / ep_count, len_sum / ep_count

@@ -34,6 +34,7 @@ from torch.distributions.normal import Normal
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from envs._gym import Box, ObservationWrapper  # noqa: E402
+from vss_amd.update import tanh_grad_bias  # noqa: E402
 
 
 def strtobool(x: str) -> bool:
@@ -143,6 +144,7 @@ class Agent(nn.Module):
 # (addmm with bias = what nn.Linear issues; dY W); only the fp32 summation order of dW differs.
 SPLITK = 64
 SPLITK_MIN_ROWS = 65536
+TANH_GRAD_COLS = (64, 128, 256, 512, 1024)  # widths vss_tanh_grad_bias takes (the Agent's: 256, 512)
 
 
 class _LinearSplitK(torch.autograd.Function):
@@ -155,23 +157,54 @@ class _LinearSplitK(torch.autograd.Function):
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
         gx = gy.mm(weight) if ctx.needs_input_grad[0] else None
-        rows = x.shape[0]
-        if rows >= SPLITK_MIN_ROWS and rows % SPLITK == 0:
-            gw = torch.bmm(gy.reshape(SPLITK, rows // SPLITK, gy.shape[1]).transpose(1, 2),
-                           x.reshape(SPLITK, rows // SPLITK, x.shape[1])).sum(0)
-        else:
-            gw = gy.t().mm(x)
-        return gx, gw, gy.sum(0)
+        return gx, _split_k_wgrad(gy, x), gy.sum(0)
+
+
+def _split_k_wgrad(gz, x):
+    rows = x.shape[0]
+    if rows >= SPLITK_MIN_ROWS and rows % SPLITK == 0:
+        return torch.bmm(gz.reshape(SPLITK, rows // SPLITK, gz.shape[1]).transpose(1, 2),
+                         x.reshape(SPLITK, rows // SPLITK, x.shape[1])).sum(0)
+    return gz.t().mm(x)
+
+
+class _LinearTanh(torch.autograd.Function):
+    """nn.Linear followed by nn.Tanh (the Agent's hidden layers, ppo…:104-111): the same forward
+    (addmm with bias, then tanh, here in place on the addmm output); the backward takes
+    gz = gy * (1 - y^2) and the bias gradient in ONE pass (vss_tanh_grad_bias, HIP) instead of
+    torch's tanh_backward + a separate reduction, then dX and split-K dW as _LinearSplitK."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        y = torch.addmm(bias, x, weight.t()).tanh_()
+        ctx.save_for_backward(x, weight, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, y = ctx.saved_tensors
+        gz, gb = tanh_grad_bias(gy, y)
+        gx = gz.mm(weight) if ctx.needs_input_grad[0] else None
+        return gx, _split_k_wgrad(gz, x), gb
 
 
 def _mlp_forward(seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
-    for m in seq:
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, nn.Linear) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.Tanh) \
+                and m.out_features in TANH_GRAD_COLS:
+            x = _LinearTanh.apply(x, m.weight, m.bias)
+            i += 2
+            continue
         if isinstance(m, nn.Linear):
             x = _LinearSplitK.apply(x, m.weight, m.bias)
         elif isinstance(m, nn.Tanh):
             x = torch.tanh(x)
         else:
             x = m(x)
+        i += 1
     return x
 
 
@@ -415,6 +448,12 @@ def train(args):
 
     from envs.wrappers import RecordEpisodeStatisticsTorch, make_env
     unwrapped_env, envs = make_env(args)
+    video = None
+    if args.capture_video and rank == 0:  # ppo…:213-221 (GIF clips of field 0, envs/render.py)
+        from envs.render import RecordVideo
+        envs = video = RecordVideo(envs, f"{args.save_path}/{run_name}",
+                                   step_trigger=lambda step: step % args.record_video_step_frequency == 0,
+                                   video_length=100)
     envs = ExtractObsWrapper(envs)
     envs = RecordEpisodeStatisticsTorch(envs, device)
     envs.single_action_space = envs.action_space
@@ -535,6 +574,8 @@ def train(args):
         # the loss / SPS curves (what the reference sends to TensorBoard/W&B), one record per update
         with open(f"{args.save_path}/{run_name}/history.json", "w") as f:
             json.dump({"args": vars(args), "world": world, "wall_s": wall, "history": history}, f, indent=1)
+    if video is not None:
+        video.recorder.flush()  # a clip still open when training ends
     writer.close()
     return agent, history
 

@@ -43,6 +43,7 @@ esac
 case ",$STEPS," in *,ablsa,*)
   ABLATE_MODE=sa ABLATE_REPS=7 run ablate_sa 300 python tools/ablate.py
   ABLATE_MODE=full ABLATE_REPS=7 run ablate_full 300 python tools/ablate.py ;; esac
+case ",$STEPS," in *,tupd,*) run pytest_update 600 python -m pytest tests/test_update.py tests/test_ppo.py -m gpu -x -q ;; esac
 case ",$STEPS," in *,tdist,*) run pytest_dist 600 python -m pytest tests/test_dist.py -m gpu -x -q ;; esac
 case ",$STEPS," in *,amp,*) run ppo_amp 900 python rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 2 --amp bf16 --save-path /tmp/runs ;; esac
 case ",$STEPS," in *,ppoprof,*)

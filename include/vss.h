@@ -214,12 +214,12 @@ int vss_value_forward_masked(void* stream, int64_t rows, int32_t n_act, const fl
  * PPO-update helper: the backward of a hidden layer's tanh
  * (ppo_continuous_action_isaacgym.py:104-111, autograd of nn.Tanh + nn.Linear's bias) in one pass:
  *   grad_in = grad_out * (1 - y^2)             (rows, cols) row-major, y = tanh output
- *   bias_partial[c][j] = sum of grad_in[r][j] over the rows r of chunk c
- * with vss_tanh_grad_chunks(rows) chunks of consecutive rows; the bias gradient is the sum of
- * bias_partial over its chunks (caller-side, deterministic).  cols in {64, 128, 256, 512, 1024};
+ *   bias_partial[c][j] = sum of grad_in[r][j] over the rows r of part c
+ * with vss_tanh_grad_chunks(rows, cols) parts (fixed row sets, -1 for a bad size); the bias
+ * gradient is the sum of bias_partial over its parts (caller-side, deterministic).  cols in {64, 128, 256, 512, 1024};
  * every pointer 16-B aligned.  Replaces torch's tanh_backward + the bias-gradient reduction.
  * ------------------------------------------------------------------------------------------- */
-int64_t vss_tanh_grad_chunks(int64_t rows);
+int64_t vss_tanh_grad_chunks(int64_t rows, int32_t cols);
 int vss_tanh_grad_bias(void* stream, int64_t rows, int32_t cols, const float* grad_out, const float* y,
                        float* grad_in, float* bias_partial);
 

@@ -95,7 +95,7 @@ def load() -> ctypes.CDLL:
     L.vss_value_forward_masked.restype = ctypes.c_int
     L.vss_episode_stats.argtypes = [P, i64] + [P] * 7
     L.vss_episode_stats.restype = ctypes.c_int
-    L.vss_tanh_grad_chunks.argtypes = [i64]
+    L.vss_tanh_grad_chunks.argtypes = [i64, i32]
     L.vss_tanh_grad_chunks.restype = i64
     L.vss_tanh_grad_bias.argtypes = [P, i64, i32, P, P, P, P]
     L.vss_tanh_grad_bias.restype = ctypes.c_int

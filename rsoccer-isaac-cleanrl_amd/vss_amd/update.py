@@ -32,7 +32,7 @@ def tanh_grad_bias(gy: torch.Tensor, y: torch.Tensor):
     gy = gy.contiguous()
     y = y.contiguous()
     gz = torch.empty_like(y)
-    partial = torch.empty((lib.vss_tanh_grad_chunks(rows), cols), device=y.device, dtype=torch.float32)
+    partial = torch.empty((lib.vss_tanh_grad_chunks(rows, cols), cols), device=y.device, dtype=torch.float32)
     N.check(lib.vss_tanh_grad_bias(N.stream_of(y.device), rows, cols, gy.data_ptr(), y.data_ptr(), gz.data_ptr(),
                                    partial.data_ptr()), "vss_tanh_grad_bias")
     return gz, partial.sum(0)

@@ -223,6 +223,31 @@ int64_t vss_tanh_grad_chunks(int64_t rows, int32_t cols);
 int vss_tanh_grad_bias(void* stream, int64_t rows, int32_t cols, const float* grad_out, const float* y,
                        float* grad_in, float* bias_partial);
 
+/*
+ * The forward of a hidden layer (nn.Linear then nn.Tanh, ppo…:104-111; in the update:
+ * ppo…:331 → Agent.get_action_and_value) in one launch on the fp32 matrix cores:
+ * y = tanh(x W^T + b) with x (rows, k_in), W (n_out, k_in) (nn.Linear's layout), both row-major,
+ * y (rows, n_out).  k_in % 4 == 0, n_out % 128 == 0; x, W, y 16-B aligned.  Replaces torch's
+ * addmm + tanh (the activation is written once instead of written, read and written again).
+ */
+int vss_linear_tanh(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
+                    const float* bias, float* y);
+
+/*
+ * The backward through a layer and the tanh below it (autograd of nn.Linear → nn.Tanh,
+ * ppo…:104-111, in loss.backward() at ppo…:357) in one launch on the fp32 matrix cores:
+ *   grad_in = (grad_next W_next) * (1 - y^2),   bias_partial[c][j] = sum of grad_in[r][j] over part c
+ * grad_next (rows, k_next) = the pre-activation gradient of the layer above, w_next_t (n_out, k_next)
+ * = that layer's weight TRANSPOSED (row-major), y (rows, n_out) = this layer's tanh output,
+ * grad_in (rows, n_out) = this layer's pre-activation gradient.  The bias gradient is the sum over
+ * the vss_linear_tanh_backward_chunks(rows, k_next, n_out) parts (fixed, deterministic; -1 for a bad
+ * shape).  k_next % 4 == 0, n_out % 128 == 0; every pointer 16-B aligned.  Replaces torch's dX GEMM +
+ * vss_tanh_grad_bias (the gradient is written once instead of written, read and written again).
+ */
+int64_t vss_linear_tanh_backward_chunks(int64_t rows, int32_t k_next, int32_t n_out);
+int vss_linear_tanh_backward(void* stream, int64_t rows, int32_t k_next, int32_t n_out, const float* grad_next,
+                             const float* w_next_t, const float* y, float* grad_in, float* bias_partial);
+
 /* ---------------------------------------------------------------------------------------------
  * Episode statistics: RecordEpisodeStatisticsTorch.step (envs/wrappers.py:66-87)
  * for `rows` learner rows in one launch, in the reference's order:

@@ -1,12 +1,15 @@
-// vss_update.hip — PPO-update helper on gfx950 (ppo_continuous_action_isaacgym.py:306-353).
+// vss_update.hip — PPO-update helpers on gfx950 (ppo_continuous_action_isaacgym.py:306-353).
 //
-// The update back-propagates through the Agent's tanh MLPs (ppo…:104-125).  For each hidden
-// layer torch issues two memory-bound passes over the (rows x cols) gradient: tanh_backward
-// (gz = gy * (1 - y^2): read gy, y, write gz) and the bias gradient (db = sum over rows of gz:
-// read gz again).  This kernel does both in one pass: every workgroup owns a fixed set of row
-// tiles, writes gz and one row of column sums; the caller reduces the (workgroups x cols)
-// partial sums (a few MB) to db.  The tile assignment and the order of the sums are fixed, so
-// db is deterministic.  HBM bytes per element: 12 (gy, y read, gz write) instead of 16.
+// 1. vss_tanh_grad_bias: the backward of a hidden tanh layer as one memory-bound pass.
+//    The update back-propagates through the Agent's tanh MLPs (ppo…:104-125).  For each hidden
+//    layer torch issues two memory-bound passes over the (rows x cols) gradient: tanh_backward
+//    (gz = gy * (1 - y^2): read gy, y, write gz) and the bias gradient (db = sum over rows of gz:
+//    read gz again).  This kernel does both in one pass: every workgroup owns a fixed set of row
+//    tiles, writes gz and one row of column sums; the caller reduces the (workgroups x cols)
+//    partial sums (a few MB) to db.  The tile assignment and the order of the sums are fixed, so
+//    db is deterministic.  HBM bytes per element: 12 (gy, y read, gz write) instead of 16.
+// 2. vss_linear_tanh / vss_linear_tanh_backward: the hidden layers' GEMMs on the fp32 matrix cores
+//    with the elementwise work in their epilogues (below).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -116,11 +119,259 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, VSS
 
 }  // namespace vupd
 
+// ---- the hidden layers' GEMMs with fused epilogues, fp32 matrix cores --------------------------------
+// out = A B^T with A (rows, K) row-major and B (n, K) row-major (nn.Linear's weight layout), both
+// K-contiguous, and one of two epilogues:
+//   EPI_TANH   (forward, ppo…:104-111 nn.Linear then nn.Tanh):  out = tanh(acc + bias)
+//              — one launch instead of hipBLASLt's addmm plus torch's tanh pass (which re-reads and
+//              re-writes the whole activation);
+//   EPI_DTANH  (backward through the NEXT layer and this layer's tanh): with A = the next layer's
+//              pre-activation gradient and B = the next layer's weight transposed,
+//              out = acc * (1 - y^2) (y = this layer's tanh output) and per-block column sums of out
+//              (the bias gradient) — instead of addmm's gy write plus vss_tanh_grad_bias's pass.
+// Block tile 128 x 128, K tiles of 32 through a double-buffered LDS image (register staging: the
+// next K tile's global loads are in flight during this K tile's MFMAs; one barrier per K tile);
+// 4 waves as 2 x 2, each a 64 x 64 output = 2 x 2 tiles of v_mfma_f32_32x32x2_f32 (exact fp32 FMA
+// chains).  k order: lane half h of a 32x32x2 step takes k = 16h + 4q + s of the 32-wide tile
+// (q = 0..3 float4 groups, s = 0..3), so each operand fragment is one ds_read_b128 per 4 k-steps;
+// rows padded to 36 floats: conflict-free for the ds_read_b128 lane groups.
+//
+// Persistent: a block walks the output tiles slot, slot + G, slot + 2G, ... (G = gridDim.x, two
+// blocks per CU), and its K tiles form one flat pipeline across tile boundaries (the next tile's
+// first K tile is fetched while this tile's last one is multiplied; the epilogue's stores drain
+// while the next tile's MFMAs run).  Slots are XCD-aware: block b runs on XCD b % 8 and takes slot
+// (b % 8) G/8 + b / 8, so the n/128 column tiles of a row band are computed at the same time on
+// ONE XCD and share the A rows through its L2.  G is a multiple of n/128, so a block always owns
+// the same column tile: its bias-gradient column sums stay in registers over all its tiles.
+namespace vgemm {
+
+#ifndef VSS_LT_EPI
+#define VSS_LT_EPI 0
+#endif
+#ifndef VSS_LT_PERSIST
+#define VSS_LT_PERSIST 1
+#endif
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+enum { EPI_TANH = 0, EPI_DTANH = 1 };
+
+// tanh(z): odd Taylor polynomial to z^9 for |z| < 0.3 (truncation < 0.6 ulp there; the exponential
+// form below would cancel in 1 - t), else sign(z) (1 - t) / (1 + t), t = 2^(-2|z| log2 e), on the
+// hardware exp2 / rcp.  Within a few ulp of tanhf (tests/test_update.py).
+__device__ __forceinline__ float tanh_f32(float z) {
+  const float a = fabsf(z), s = z * z;
+  const float poly = z + z * s * (-0.333333343f + s * (0.133333340f + s * (-0.0539682545f + s * 0.0218694885f)));
+  const float t = __builtin_amdgcn_exp2f(-2.8853900817779268f * a);
+  const float ex = copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), z);
+#ifdef VSS_LT_TANH_FAST  // profiling knob: the exponential form only
+  (void)poly;
+  return ex;
+#else
+  return a < 0.3f ? poly : ex;
+#endif
+}
+
+constexpr int kBM = 128, kBN = 128, kKS = 32, kLS = kKS + 4, kThreadsG = 256;
+constexpr int kTM = kBM / 64, kTN = kBN / 64;  // 32 x 32 tiles per wave (waves as 2 x 2)
+constexpr int kLdsFloats = 2 * (kBM + kBN) * kLS;
+constexpr int kBlocksPerCu = 2;  // 2 blocks per CU fit the LDS (72 KB each): 2 waves per SIMD
+constexpr int kRA = kBM * kKS / 4 / kThreadsG, kRB = kBN * kKS / 4 / kThreadsG;  // float4 staged per thread
+
+struct GemmArgs {
+  int64_t rows;
+  int32_t n, k;
+  const float* a;     // (rows, k)
+  const float* b;     // (n, k)
+  const float* bias;  // EPI_TANH: (n)
+  const float* y;     // EPI_DTANH: (rows, n), the tanh output the gradient passes through
+  float* out;         // (rows, n)
+  float* partial;     // EPI_DTANH: (G / (n / kBN), n) column sums of out
+  int64_t tiles;      // ceil(rows / kBM) * (n / kBN) output tiles, row band major
+};
+
+template <int EPI>
+__global__ __launch_bounds__(kThreadsG, kBlocksPerCu) void gemm_kernel(GemmArgs p) {
+  __shared__ float lds[kLdsFloats];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
+  const int nb = p.n / kBN;
+  const int K = p.k, ktiles = (K + kKS - 1) / kKS;
+  const int64_t M = p.rows;
+  const int G = gridDim.x;
+  const int64_t slot = (G % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
+  if (slot >= p.tiles) return;  // whole block (the host sizes G <= tiles)
+  int64_t tile = slot;
+
+  f32x16 acc[kTM][kTN];
+  float csum[kTN] = {0.0f, 0.0f};  // EPI_DTANH: this lane's column sums over all its tiles
+  float4 ra[kRA], rb[kRB];
+  auto gload = [&](int64_t t, int kt) {
+    const int64_t row0 = (t / nb) * kBM;
+    const int col0 = (int)(t % nb) * kBN;
+#pragma unroll
+    for (int i = 0; i < kRA; ++i) {
+      const int idx = tid + i * kThreadsG, r = idx >> 3, c = (idx & 7) * 4, kk = kt * kKS + c;
+      const int64_t gr = row0 + r;
+      ra[i] = (gr < M && kk < K) ? *reinterpret_cast<const float4*>(p.a + gr * K + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < kRB; ++i) {
+      const int idx = tid + i * kThreadsG, r = idx >> 3, c = (idx & 7) * 4, kk = kt * kKS + c;
+      rb[i] = kk < K ? *reinterpret_cast<const float4*>(p.b + (int64_t)(col0 + r) * K + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto swrite = [&](int buf) {
+    float* As = lds + buf * (kBM + kBN) * kLS;
+    float* Bs = As + kBM * kLS;
+#pragma unroll
+    for (int i = 0; i < kRA; ++i) {
+      const int idx = tid + i * kThreadsG;
+      *reinterpret_cast<float4*>(As + (idx >> 3) * kLS + (idx & 7) * 4) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < kRB; ++i) {
+      const int idx = tid + i * kThreadsG;
+      *reinterpret_cast<float4*>(Bs + (idx >> 3) * kLS + (idx & 7) * 4) = rb[i];
+    }
+  };
+
+  gload(tile, 0);
+  swrite(0);
+  __syncthreads();
+  const int r = lane & 31, h = lane >> 5;
+  int buf = 0;
+  for (;;) {
+    const int64_t next = tile + G;
+#pragma unroll
+    for (int i = 0; i < kTM; ++i)
+#pragma unroll
+      for (int j = 0; j < kTN; ++j)
+        acc[i][j] = (f32x16){0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < ktiles; ++kt) {
+      // the next K tile of the flat pipeline: this tile's kt + 1, else the next tile's first
+      const bool more = kt + 1 < ktiles || next < p.tiles;
+      if (kt + 1 < ktiles) gload(tile, kt + 1);
+      else if (more) gload(next, 0);
+      const float* As = lds + buf * (kBM + kBN) * kLS + (wm * (kBM / 2) + r) * kLS + h * 16;
+      const float* Bs = lds + buf * (kBM + kBN) * kLS + kBM * kLS + (wn * (kBN / 2) + r) * kLS + h * 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float4 a4[kTM], b4[kTN];
+#pragma unroll
+        for (int i = 0; i < kTM; ++i) a4[i] = *reinterpret_cast<const float4*>(As + i * 32 * kLS + q * 4);
+#pragma unroll
+        for (int j = 0; j < kTN; ++j) b4[j] = *reinterpret_cast<const float4*>(Bs + j * 32 * kLS + q * 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < kTM; ++i)
+#pragma unroll
+            for (int j = 0; j < kTN; ++j) {
+              const float av = s == 0 ? a4[i].x : s == 1 ? a4[i].y : s == 2 ? a4[i].z : a4[i].w;
+              const float bv = s == 0 ? b4[j].x : s == 1 ? b4[j].y : s == 2 ? b4[j].z : b4[j].w;
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+            }
+      }
+      if (more) {
+        swrite(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+      }
+    }
+
+    // epilogue, C/D map of the 32x32 tile: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+    const int64_t row0 = (tile / nb) * kBM;
+    const int col0 = (int)(tile % nb) * kBN;
+#pragma unroll
+    for (int j = 0; j < kTN; ++j) {
+      const int col = col0 + wn * (kBN / 2) + j * 32 + r;
+      const float bcol = EPI == EPI_TANH ? p.bias[col] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < kTM; ++i) {
+        const int64_t rbase = row0 + wm * (kBM / 2) + i * 32 + 4 * h;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int64_t row = rbase + (e & 3) + 8 * (e >> 2);
+          if (row < M) {
+            const int64_t o = row * p.n + col;
+            if constexpr (EPI == EPI_TANH) {
+#if VSS_LT_EPI == 2  // profiling knob: no epilogue (one store per tile keeps the MFMAs live)
+              if (e == 0) p.out[o] = acc[i][j][0] + acc[i][j][5] + acc[i][j][15] + bcol;
+#elif VSS_LT_EPI == 1  // profiling knob: bias only
+              p.out[o] = acc[i][j][e] + bcol;
+#else
+              p.out[o] = tanh_f32(acc[i][j][e] + bcol);
+#endif
+            } else {
+              const float yv = p.y[o];
+              const float g = acc[i][j][e] * fmaf(-yv, yv, 1.0f);
+              p.out[o] = g;
+              csum[j] += g;
+            }
+          }
+        }
+      }
+    }
+    if (next >= p.tiles) break;
+    tile = next;
+  }
+
+  if constexpr (EPI == EPI_DTANH) {
+    // the block's column sums: lane halves (rows 4h..), then the two row waves (wm), fixed order
+    __syncthreads();  // every wave is done with the pipeline's LDS buffers
+    float* red = lds;  // [2][kBN]
+#pragma unroll
+    for (int j = 0; j < kTN; ++j) {
+      const float v = csum[j] + __shfl_xor(csum[j], 32);
+      if (h == 0) red[wm * kBN + wn * (kBN / 2) + j * 32 + r] = v;
+    }
+    __syncthreads();
+    if (tid < kBN) p.partial[(slot / nb) * p.n + (slot % nb) * kBN + tid] = red[tid] + red[kBN + tid];
+  }
+}
+
+// CUs of the current device (cached per device; an attribute query, no synchronisation)
+static int n_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cached[dev] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+// grid: min(tiles, blocks_per_cu x CUs), the latter rounded down to a multiple of 8 (XCD slots) and
+// of n / kBN (a fixed column tile per block)
+static int64_t grid_for(int64_t tiles, int nb) {
+#if VSS_LT_PERSIST
+  int64_t g = (int64_t)n_cus() * kBlocksPerCu;
+  const int64_t q = 8 * (int64_t)nb;
+  g -= g % q;
+  if (g > 0 && g < tiles) return g;
+#else
+  (void)nb;
+#endif
+  return tiles;
+}
+
+static bool shape_ok(int64_t rows, int32_t k, int32_t n) {
+  return rows >= 0 && rows <= (int64_t(1) << 40) && k >= 4 && k % 4 == 0 && k <= 65536 && n >= kBN && n % kBN == 0 &&
+         n <= 65536 && (rows + kBM - 1) / kBM * (n / kBN) <= 0x7fffffff;
+}
+
+static int64_t tiles_for(int64_t rows, int32_t n) { return (rows + kBM - 1) / kBM * (n / kBN); }
+
+}  // namespace vgemm
+
 extern "C" {
 
 static bool tanh_grad_cols_ok(int32_t cols) {
   return cols == 64 || cols == 128 || cols == 256 || cols == 512 || cols == 1024;
 }
+
+static bool misaligned(const void* p) { return !p || (reinterpret_cast<uintptr_t>(p) & 15) != 0; }
 
 int64_t vss_tanh_grad_chunks(int64_t rows, int32_t cols) {
   return (rows < 0 || !tanh_grad_cols_ok(cols)) ? -1 : vupd::n_blocks(rows, cols);
@@ -128,8 +379,8 @@ int64_t vss_tanh_grad_chunks(int64_t rows, int32_t cols) {
 
 int vss_tanh_grad_bias(void* stream, int64_t rows, int32_t cols, const float* grad_out, const float* y,
                        float* grad_in, float* bias_partial) {
-  auto bad = [](const void* p) { return !p || (reinterpret_cast<uintptr_t>(p) & 15) != 0; };
-  if (rows < 0 || rows > (int64_t(1) << 40) || bad(grad_out) || bad(y) || bad(grad_in) || bad(bias_partial))
+  if (rows < 0 || rows > (int64_t(1) << 40) || misaligned(grad_out) || misaligned(y) || misaligned(grad_in) ||
+      misaligned(bias_partial))
     return VSS_E_ARG;
   if (!tanh_grad_cols_ok(cols)) return VSS_E_ARG;
   if (rows == 0) return VSS_OK;
@@ -146,6 +397,40 @@ int vss_tanh_grad_bias(void* stream, int64_t rows, int32_t cols, const float* gr
     case 512: hipLaunchKernelGGL(vupd::tanh_grad_bias_kernel<128>, grid, block, 0, s, rows, g4, y4, z4, p4); break;
     default: hipLaunchKernelGGL(vupd::tanh_grad_bias_kernel<256>, grid, block, 0, s, rows, g4, y4, z4, p4); break;
   }
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+}
+
+int vss_linear_tanh(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
+                    const float* bias, float* y) {
+  if (!vgemm::shape_ok(rows, k_in, n_out) || misaligned(x) || misaligned(w) || misaligned(y) || !bias)
+    return VSS_E_ARG;
+  if (rows == 0) return VSS_OK;
+  const int64_t tiles = vgemm::tiles_for(rows, n_out);
+  vgemm::GemmArgs a{rows, n_out, k_in, x, w, bias, nullptr, y, nullptr, tiles};
+  const int64_t grid = vgemm::grid_for(tiles, n_out / vgemm::kBN);
+  hipLaunchKernelGGL(vgemm::gemm_kernel<vgemm::EPI_TANH>, dim3((unsigned)grid), dim3(vgemm::kThreadsG), 0,
+                     (hipStream_t)stream, a);
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+}
+
+int64_t vss_linear_tanh_backward_chunks(int64_t rows, int32_t k_next, int32_t n_out) {
+  if (!vgemm::shape_ok(rows, k_next, n_out)) return -1;
+  if (rows == 0) return 0;
+  const int nb = n_out / vgemm::kBN;
+  return vgemm::grid_for(vgemm::tiles_for(rows, n_out), nb) / nb;
+}
+
+int vss_linear_tanh_backward(void* stream, int64_t rows, int32_t k_next, int32_t n_out, const float* grad_next,
+                             const float* w_next_t, const float* y, float* grad_in, float* bias_partial) {
+  if (!vgemm::shape_ok(rows, k_next, n_out) || misaligned(grad_next) || misaligned(w_next_t) || misaligned(y) ||
+      misaligned(grad_in) || misaligned(bias_partial))
+    return VSS_E_ARG;
+  if (rows == 0) return VSS_OK;
+  const int64_t tiles = vgemm::tiles_for(rows, n_out);
+  vgemm::GemmArgs a{rows, n_out, k_next, grad_next, w_next_t, nullptr, y, grad_in, bias_partial, tiles};
+  const int64_t grid = vgemm::grid_for(tiles, n_out / vgemm::kBN);
+  hipLaunchKernelGGL(vgemm::gemm_kernel<vgemm::EPI_DTANH>, dim3((unsigned)grid), dim3(vgemm::kThreadsG), 0,
+                     (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 

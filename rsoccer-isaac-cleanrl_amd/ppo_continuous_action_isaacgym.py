@@ -34,7 +34,7 @@ from torch.distributions.normal import Normal
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from envs._gym import Box, ObservationWrapper  # noqa: E402
-from vss_amd.update import tanh_grad_bias  # noqa: E402
+from vss_amd.update import gemm_shape_ok, linear_tanh, linear_tanh_backward, tanh_grad_bias  # noqa: E402
 
 
 def strtobool(x: str) -> bool:
@@ -188,7 +188,69 @@ class _LinearTanh(torch.autograd.Function):
         return gx, _split_k_wgrad(gz, x), gb
 
 
+class _TanhMLP(torch.autograd.Function):
+    """The Agent's MLP (ppo…:104-111: (Linear, Tanh) x L + Linear) as ONE autograd node for the
+    update.  Forward: each hidden layer is vss_linear_tanh (GEMM + bias + tanh in one fp32 MFMA
+    launch); the output layer is addmm, as nn.Linear issues.  Backward: the output layer's input
+    gradient (a few columns) by torch's mm + the one-pass vss_tanh_grad_bias; every other hidden
+    tanh by vss_linear_tanh_backward (the input-gradient GEMM of the layer above with the tanh
+    derivative and the bias-gradient column sums in its epilogue); weight gradients split-K as
+    _LinearSplitK.  Inputs: x, W_0, b_0, ..., W_L, b_L."""
+
+    @staticmethod
+    def forward(ctx, x, *params):
+        ws, bs = params[0::2], params[1::2]
+        hs = [x]
+        for w, b in zip(ws[:-1], bs[:-1]):
+            hs.append(linear_tanh(hs[-1], w, b))
+        ctx.save_for_backward(*hs, *ws)
+        return torch.addmm(bs[-1], hs[-1], ws[-1].t())
+
+    @staticmethod
+    def backward(ctx, gout):
+        saved = ctx.saved_tensors
+        n = len(saved) // 2
+        hs, ws = saved[:n], saved[n:]  # hs[l] = input of layer l (hs[0] = x), ws[l] = its weight
+        grads = [None] * (2 * n)
+        gz = gout.contiguous()  # pre-activation gradient of the current layer
+        gb = gz.sum(0)
+        for layer in reversed(range(n)):
+            grads[2 * layer], grads[2 * layer + 1] = _split_k_wgrad(gz, hs[layer]), gb
+            if layer == 0:
+                break
+            if layer == n - 1:
+                gz, gb = tanh_grad_bias(gz.mm(ws[layer]), hs[layer])
+            else:
+                gz, gb = linear_tanh_backward(gz, ws[layer], hs[layer])
+        gx = gz.mm(ws[0]) if ctx.needs_input_grad[0] else None
+        return (gx, *grads)
+
+
+# the update's MLP path: "split" (default) = _LinearTanh / _LinearSplitK (hipBLASLt GEMMs + the
+# one-pass HIP tanh backward); "fused" = _TanhMLP (our fp32 MFMA GEMMs with the tanh work in their
+# epilogues).  "fused" saves the elementwise passes but its GEMM body runs at 83-117 TF against
+# hipBLASLt's 133-144 TF on these shapes, so it is slower end to end (DESIGN.md §5.3,
+# profiles/r01_gemm_fused_bench.log); opt in with VSS_UPDATE_MLP=fused.
+UPDATE_MLP = os.environ.get("VSS_UPDATE_MLP", "split")
+
+
+def _fused_mlp_ok(seq: nn.Sequential) -> bool:
+    mods = list(seq)
+    if len(mods) < 3 or len(mods) % 2 == 0:
+        return False
+    lins, acts = mods[0::2], mods[1::2]
+    if not all(type(m) is nn.Linear and m.bias is not None for m in lins) or \
+            not all(isinstance(a, nn.Tanh) for a in acts):
+        return False
+    return all(gemm_shape_ok(m.in_features, m.out_features) for m in lins[:-1]) and \
+        all(gemm_shape_ok(m.out_features, m.in_features) for m in lins[1:-1]) and \
+        lins[-1].in_features in TANH_GRAD_COLS
+
+
 def _mlp_forward(seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+    if UPDATE_MLP == "fused" and x.dtype == torch.float32 and _fused_mlp_ok(seq):
+        params = [t for m in list(seq)[0::2] for t in (m.weight, m.bias)]
+        return _TanhMLP.apply(x, *params)
     mods = list(seq)
     i = 0
     while i < len(mods):
@@ -209,8 +271,9 @@ def _mlp_forward(seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
 
 
 def get_action_and_value_update(agent: "Agent", x, action):
-    """Agent.get_action_and_value (ppo…:157-164) on the same parameters, for the PPO update:
-    identical forward, split-K weight gradients in the backward."""
+    """Agent.get_action_and_value (ppo…:157-164) on the same parameters, for the PPO update: the
+    same function (forward within fp32 rounding: fused GEMM summation order and a few-ulp tanh),
+    the MLPs through _TanhMLP, split-K weight gradients in the backward."""
     mean = _mlp_forward(agent.actor_mean, x)
     std = torch.exp(agent.actor_logstd.expand_as(mean))
     probs = Normal(mean, std)

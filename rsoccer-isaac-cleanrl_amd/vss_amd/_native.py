@@ -25,7 +25,8 @@ CH_BALL_X, CH_BALL_Y, CH_BALL_VX, CH_BALL_VY = 0, 1, 2, 3
 CH_RX, CH_RY, CH_RQX, CH_RQY, CH_RQZ, CH_RQW, CH_RVX, CH_RVY, CH_RW = 4, 10, 16, 22, 28, 34, 40, 46, 52
 EXPORTED = ("vss_abi_version", "vss_error_string", "vss_step", "vss_rollout", "vss_reset_dones",
             "vss_compute_observations", "vss_mlp_packed_size", "vss_mlp_pack", "vss_policy_forward",
-            "vss_value_forward_masked", "vss_episode_stats", "vss_tanh_grad_chunks", "vss_tanh_grad_bias")
+            "vss_value_forward_masked", "vss_episode_stats", "vss_tanh_grad_chunks", "vss_tanh_grad_bias",
+            "vss_linear_tanh", "vss_linear_tanh_backward_chunks", "vss_linear_tanh_backward")
 
 
 class VssParams(ctypes.Structure):
@@ -99,6 +100,12 @@ def load() -> ctypes.CDLL:
     L.vss_tanh_grad_chunks.restype = i64
     L.vss_tanh_grad_bias.argtypes = [P, i64, i32, P, P, P, P]
     L.vss_tanh_grad_bias.restype = ctypes.c_int
+    L.vss_linear_tanh.argtypes = [P, i64, i32, i32, P, P, P, P]
+    L.vss_linear_tanh.restype = ctypes.c_int
+    L.vss_linear_tanh_backward_chunks.argtypes = [i64, i32, i32]
+    L.vss_linear_tanh_backward_chunks.restype = i64
+    L.vss_linear_tanh_backward.argtypes = [P, i64, i32, i32, P, P, P, P, P]
+    L.vss_linear_tanh_backward.restype = ctypes.c_int
     if L.vss_abi_version() != ABI_VERSION:
         raise NativeError(f"libvss_amd ABI {L.vss_abi_version()} != expected {ABI_VERSION}")
     _lib = L

@@ -1,12 +1,17 @@
-"""PPO-update helper: the backward of a hidden tanh layer in one HIP pass
-(csrc/vss_update.hip, include/vss.h `vss_tanh_grad_bias`).
+"""PPO-update helpers (csrc/vss_update.hip, include/vss.h):
 
-    gz, db = tanh_grad_bias(gy, y)   # gz = gy * (1 - y^2), db = gz.sum(0)
+    gz, db = tanh_grad_bias(gy, y)                # gz = gy * (1 - y^2), db = gz.sum(0)
+    y = linear_tanh(x, w, b)                      # tanh(x @ w.T + b)
+    gz, db = linear_tanh_backward(gz_next, w_next, y)
+                                                  # gz = (gz_next @ w_next) * (1 - y^2), db = gz.sum(0)
 
-replaces torch's tanh_backward + the bias-gradient reduction that autograd issues for
-nn.Tanh -> nn.Linear (ppo_continuous_action_isaacgym.py:104-111).  On a ROCm device it runs the
-HIP kernel (and raises if the library is missing); CPU tensors (the CPU test suite's PPO loop)
-take the same formula in torch.
+They replace what autograd issues for the Agent's nn.Linear -> nn.Tanh pairs
+(ppo_continuous_action_isaacgym.py:104-111): tanh_backward + the bias-gradient reduction
+(vss_tanh_grad_bias), addmm + tanh (vss_linear_tanh: one fp32 MFMA GEMM with bias and tanh in its
+epilogue), and the input-gradient GEMM of the layer above + tanh_backward + bias reduction
+(vss_linear_tanh_backward: one fp32 MFMA GEMM with the tanh derivative and the column sums in its
+epilogue).  On a ROCm device they run the HIP kernels (and raise if the library is missing); CPU
+tensors (the CPU test suite's PPO loop) take the same formulas in torch.
 """
 from __future__ import annotations
 
@@ -35,4 +40,66 @@ def tanh_grad_bias(gy: torch.Tensor, y: torch.Tensor):
     partial = torch.empty((lib.vss_tanh_grad_chunks(rows, cols), cols), device=y.device, dtype=torch.float32)
     N.check(lib.vss_tanh_grad_bias(N.stream_of(y.device), rows, cols, gy.data_ptr(), y.data_ptr(), gz.data_ptr(),
                                    partial.data_ptr()), "vss_tanh_grad_bias")
+    return gz, partial.sum(0)
+
+
+def gemm_shape_ok(k: int, n: int) -> bool:
+    """Shapes the fused GEMMs take: contraction k % 4 == 0, output width n % 128 == 0."""
+    return k >= 4 and k % 4 == 0 and n >= 128 and n % 128 == 0
+
+
+def _fp32_2d(name, *ts):
+    for t in ts:
+        if t.dtype != torch.float32:
+            raise ValueError(f"{name}: fp32 tensors only, got {t.dtype}")
+
+
+def linear_tanh(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """tanh(x @ w.T + b) for x (rows, k), w (n, k) (nn.Linear's weight), b (n,)."""
+    if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1] or b.shape != (w.shape[0],):
+        raise ValueError(f"linear_tanh: x {tuple(x.shape)}, w {tuple(w.shape)}, b {tuple(b.shape)}")
+    if x.device.type != "cuda":
+        return torch.addmm(b, x, w.t()).tanh_()
+    rows, k = x.shape
+    n = w.shape[0]
+    _fp32_2d("vss_linear_tanh", x, w, b)
+    if not gemm_shape_ok(k, n):
+        raise ValueError(f"vss_linear_tanh: k % 4 == 0 and n % 128 == 0 required, got k={k}, n={n}")
+    lib = N.load()
+    y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
+    if rows == 0:
+        return y
+    x, w, b = x.contiguous(), w.contiguous(), b.contiguous()
+    N.check(lib.vss_linear_tanh(N.stream_of(x.device), rows, k, n, x.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                y.data_ptr()), "vss_linear_tanh")
+    return y
+
+
+def linear_tanh_backward(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.Tensor):
+    """The pre-activation gradient of a tanh layer from the one of the layer above:
+    gz = (gz_next @ w_next) * (1 - y^2) and db = gz.sum(0), with gz_next (rows, k_next), w_next
+    (k_next, n) (the next layer's nn.Linear weight), y (rows, n) (this layer's tanh output)."""
+    if gz_next.dim() != 2 or w_next.dim() != 2 or y.dim() != 2 or gz_next.shape[0] != y.shape[0] \
+            or w_next.shape != (gz_next.shape[1], y.shape[1]):
+        raise ValueError(f"linear_tanh_backward: gz_next {tuple(gz_next.shape)}, w_next {tuple(w_next.shape)}, "
+                         f"y {tuple(y.shape)}")
+    if gz_next.device.type != "cuda":
+        gz = gz_next.mm(w_next) * (1.0 - y * y)
+        return gz, gz.sum(0)
+    rows, k_next = gz_next.shape
+    n = y.shape[1]
+    _fp32_2d("vss_linear_tanh_backward", gz_next, w_next, y)
+    if not gemm_shape_ok(k_next, n):
+        raise ValueError(f"vss_linear_tanh_backward: k_next % 4 == 0 and n % 128 == 0 required, got {k_next}, {n}")
+    lib = N.load()
+    gz = torch.empty((rows, n), device=y.device, dtype=torch.float32)
+    if rows == 0:
+        return gz, torch.zeros(n, device=y.device, dtype=torch.float32)
+    gz_next, y = gz_next.contiguous(), y.contiguous()
+    w_t = w_next.t().contiguous()  # (n, k_next): the kernel's K-contiguous operand layout
+    partial = torch.empty((lib.vss_linear_tanh_backward_chunks(rows, k_next, n), n), device=y.device,
+                          dtype=torch.float32)
+    N.check(lib.vss_linear_tanh_backward(N.stream_of(y.device), rows, k_next, n, gz_next.data_ptr(), w_t.data_ptr(),
+                                         y.data_ptr(), gz.data_ptr(), partial.data_ptr()),
+            "vss_linear_tanh_backward")
     return gz, partial.sum(0)

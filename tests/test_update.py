@@ -1,12 +1,13 @@
-"""PPO-update helper vss_tanh_grad_bias (csrc/vss_update.hip): one HIP pass for the backward of a
-hidden tanh layer, checked against torch's tanh_backward + bias-gradient reduction (the fp32
-reference of the same op), and the update's gradients through it against plain autograd."""
+"""PPO-update helpers (csrc/vss_update.hip): vss_tanh_grad_bias (one HIP pass for the backward of a
+hidden tanh layer) against torch's tanh_backward + bias-gradient reduction (the fp32 reference of
+the same op); the fused-epilogue GEMMs vss_linear_tanh / vss_linear_tanh_backward against torch
+fp32 and fp64; and the update's gradients through either path against plain autograd."""
 import pytest
 import torch
 
 import ppo_continuous_action_isaacgym as P
 from vss_amd import _native as N
-from vss_amd.update import tanh_grad_bias
+from vss_amd.update import linear_tanh, linear_tanh_backward, tanh_grad_bias
 
 from test_ppo import make_agent
 
@@ -52,11 +53,120 @@ def test_tanh_grad_bias_refusals_gpu():
                                   buf.data_ptr(), part.data_ptr()) != 0
 
 
+def test_cpu_fused_layer_formulas_match_autograd():
+    """The CPU forms of linear_tanh / linear_tanh_backward (what the CPU suite's PPO loop runs) are
+    autograd's nn.Linear -> nn.Tanh -> nn.Linear chain."""
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(40, 52, generator=g)
+    w0, b0 = torch.randn(256, 52, generator=g) * 0.1, torch.randn(256, generator=g) * 0.1
+    w1 = (torch.randn(128, 256, generator=g) * 0.1).requires_grad_()
+    gout = torch.randn(40, 128, generator=g)
+    z0 = torch.addmm(b0, x, w0.t()).requires_grad_()
+    y0 = torch.tanh(z0)
+    (ref,) = torch.autograd.grad(y0.mm(w1.t()), z0, gout)
+    torch.testing.assert_close(linear_tanh(x, w0, b0), y0.detach(), rtol=0, atol=0)
+    gz, db = linear_tanh_backward(gout, w1.detach(), y0.detach())
+    torch.testing.assert_close(gz, ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(db, ref.sum(0), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("mlp", ["fused", "split"])
+def test_update_mlp_paths_cpu_match_autograd(mlp, monkeypatch):
+    """Both update MLP paths (the _TanhMLP node and the per-layer functions) on CPU tensors: the
+    Agent's outputs and autograd's gradients."""
+    monkeypatch.setattr(P, "UPDATE_MLP", mlp)
+    agent = make_agent(2)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(96, 52, generator=g)
+    a = torch.randn(96, 2, generator=g) * 0.5
+    outs_ref = agent.get_action_and_value(x, a)
+    grads_ref = torch.autograd.grad(outs_ref[1].sum() + outs_ref[2].sum() + outs_ref[3].sum(), list(agent.parameters()))
+    outs = P.get_action_and_value_update(agent, x, a)
+    for u, v in zip(outs[1:], outs_ref[1:]):
+        torch.testing.assert_close(u, v, rtol=1e-6, atol=1e-6)
+    grads = torch.autograd.grad(outs[1].sum() + outs[2].sum() + outs[3].sum(), list(agent.parameters()))
+    for (name, _), u, v in zip(agent.named_parameters(), grads, grads_ref):
+        torch.testing.assert_close(u, v, rtol=1e-4, atol=1e-4 * float(v.abs().max()) + 1e-7, msg=name)
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("k,n", [(52, 256), (256, 512), (512, 512), (512, 256), (8, 128)])
+@pytest.mark.parametrize("rows", [1, 127, 129, 4133, 70_000])
+def test_linear_tanh_gpu(rows, k, n):
+    """vss_linear_tanh vs the fp32 torch op (addmm + tanh) and an fp64 reference: the fused GEMM
+    sums in a different order and its tanh is within a few ulp, so within fp32 GEMM rounding."""
+    g = torch.Generator(device="cuda").manual_seed(rows + 7 * k + n)
+    x = torch.tanh(torch.randn(rows, k, device="cuda", generator=g))
+    w = torch.randn(n, k, device="cuda", generator=g) * (2.0 / k) ** 0.5
+    b = torch.randn(n, device="cuda", generator=g) * 0.1
+    y = linear_tanh(x, w, b)
+    ref64 = torch.tanh(x.double() @ w.double().t() + b.double())
+    ref32 = torch.addmm(b, x, w.t()).tanh_()
+    # fp32 GEMM error bound ~ k * eps * sum|x w| (sum|x w| <= sqrt(2k) here) + a few ulp of tanh
+    tol = 4e-7 * (k * (2.0 * k) ** 0.5) ** 0.5 + 1e-6
+    assert float((y.double() - ref64).abs().max()) < tol
+    assert float((y - ref32).abs().max()) < 2 * tol
+    assert y.shape == (rows, n) and bool(torch.isfinite(y).all())
+
+
+@pytest.mark.gpu
+def test_linear_tanh_small_arguments_keep_relative_precision_gpu():
+    """The tanh epilogue keeps relative precision near 0 (odd polynomial for |z| < 0.3, where the
+    exponential form would cancel) and saturates cleanly at large |z|."""
+    z = torch.cat([torch.logspace(-30, 1.5, 20000, device="cuda"), torch.tensor([0.0, 9.0, 20.0, 88.0], device="cuda")])
+    z = torch.cat([z, -z])
+    rows = z.numel()
+    x = torch.zeros(rows, 4, device="cuda")
+    x[:, 0] = z
+    w = torch.zeros(128, 4, device="cuda")
+    w[:, 0] = 1.0
+    y = linear_tanh(x, w, torch.zeros(128, device="cuda"))[:, 0].double()
+    ref = torch.tanh(z.double())
+    rel = ((y - ref).abs() / ref.abs().clamp_min(1e-38)).max()
+    assert float(rel) < 1e-6, float(rel)  # <= 8 ulp; the cancelling form gives ~1e-3 at z = 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k_next,n", [(256, 512), (512, 512), (512, 256), (4, 128)])
+@pytest.mark.parametrize("rows", [1, 127, 129, 4133, 70_000])
+def test_linear_tanh_backward_gpu(rows, k_next, n):
+    """vss_linear_tanh_backward vs fp64: gz = (gz_next @ w_next) * (1 - y^2) and db = gz.sum(0);
+    deterministic (the same call twice gives the same bits)."""
+    g = torch.Generator(device="cuda").manual_seed(rows * 3 + k_next + n)
+    gn = torch.randn(rows, k_next, device="cuda", generator=g) * 1e-3
+    wn = torch.randn(k_next, n, device="cuda", generator=g) * (1.0 / k_next) ** 0.5
+    y = torch.tanh(torch.randn(rows, n, device="cuda", generator=g) * 2)
+    gz, db = linear_tanh_backward(gn, wn, y)
+    ref = (gn.double() @ wn.double()) * (1 - y.double() ** 2)
+    scale = float((gn.double().abs() @ wn.double().abs()).max())
+    assert float((gz.double() - ref).abs().max()) < 1.2e-7 * k_next * scale + 1e-12  # ~ 2 k u sum|g w|
+    torch.testing.assert_close(db.double(), ref.sum(0), rtol=1e-5, atol=1e-6 * scale * (rows ** 0.5 + 1))
+    gz2, db2 = linear_tanh_backward(gn, wn, y)
+    assert torch.equal(gz, gz2) and torch.equal(db, db2)
+
+
+@pytest.mark.gpu
+def test_fused_gemm_refusals_gpu():
+    lib = N.load()
+    buf = torch.zeros(1 << 16, device="cuda")
+    p, s = buf.data_ptr(), N.stream_of(buf.device)
+    assert lib.vss_linear_tanh(s, 4, 8, 100, p, p, p, p) != 0  # n % 128
+    assert lib.vss_linear_tanh(s, 4, 6, 128, p, p, p, p) != 0  # k % 4
+    assert lib.vss_linear_tanh(s, 4, 8, 128, p + 4, p, p, p) != 0  # misaligned
+    assert lib.vss_linear_tanh_backward(s, 4, 8, 128, p, p, p, p, None) != 0
+    assert lib.vss_linear_tanh_backward_chunks(4, 8, 100) == -1
+    with pytest.raises(ValueError):
+        linear_tanh(buf[:64].view(8, 8), buf[:800].view(100, 8), buf[:100])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mlp", ["fused", "split"])
 @pytest.mark.parametrize("rows", [256, 65536 + 64 * 3])
-def test_update_gradients_through_hip_match_autograd_gpu(rows):
-    """The update's forward (addmm + in-place tanh) equals the Agent's; its gradients (HIP tanh
-    backward + bias, split-K dW) equal autograd's up to fp32 summation order."""
+def test_update_gradients_through_hip_match_autograd_gpu(rows, mlp, monkeypatch):
+    """The update's forward equals the Agent's (bit for bit on the hipBLASLt path "split"; within
+    fp32 GEMM rounding on the fused-GEMM path); its gradients (fused HIP GEMM epilogues or the HIP
+    tanh backward + bias, split-K dW) equal autograd's up to fp32 summation order."""
+    monkeypatch.setattr(P, "UPDATE_MLP", mlp)
     agent = make_agent(2).cuda()
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.randn(rows, 52, device="cuda", generator=g)
@@ -65,8 +175,9 @@ def test_update_gradients_through_hip_match_autograd_gpu(rows):
     loss_ref = outs_ref[1].sum() + outs_ref[2].sum() + outs_ref[3].sum()
     grads_ref = torch.autograd.grad(loss_ref, list(agent.parameters()))
     outs = P.get_action_and_value_update(agent, x, a)
+    tol = 0 if mlp == "split" else 2e-5
     for u, v in zip(outs[1:], outs_ref[1:]):
-        torch.testing.assert_close(u, v, rtol=0, atol=0)
+        torch.testing.assert_close(u, v, rtol=tol, atol=tol)
     loss = outs[1].sum() + outs[2].sum() + outs[3].sum()
     grads = torch.autograd.grad(loss, list(agent.parameters()))
     for (name, _), u, v in zip(agent.named_parameters(), grads, grads_ref):

@@ -44,6 +44,13 @@ case ",$STEPS," in *,ablsa,*)
   ABLATE_MODE=sa ABLATE_REPS=7 run ablate_sa 300 python tools/ablate.py
   ABLATE_MODE=full ABLATE_REPS=7 run ablate_full 300 python tools/ablate.py ;; esac
 case ",$STEPS," in *,tupd,*) run pytest_update 600 python -m pytest tests/test_update.py tests/test_ppo.py -m gpu -x -q ;; esac
+# the update's fused-epilogue GEMMs: unit tests, kernel bench vs torch, PPO update fused vs split
+case ",$STEPS," in *,gemm,*)
+  run pytest_update 500 python -u -m pytest tests/test_update.py -m gpu -x -v --timeout 120 --timeout-method thread
+  run gemm_fused 300 python -u tools/gemm_fused_bench.py
+  VSS_UPDATE_MLP=fused run ppo_fused 300 python -u rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 3 --log false
+  VSS_UPDATE_MLP=split run ppo_split 300 python -u rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 3 --log false ;;
+esac
 case ",$STEPS," in *,tdist,*) run pytest_dist 600 python -m pytest tests/test_dist.py -m gpu -x -q ;; esac
 case ",$STEPS," in *,amp,*) run ppo_amp 900 python rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 2 --amp bf16 --save-path /tmp/runs ;; esac
 case ",$STEPS," in *,ppoprof,*)

@@ -142,12 +142,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, VSS
 // while the next tile's MFMAs run).  Slots are XCD-aware: block b runs on XCD b % 8 and takes slot
 // (b % 8) G/8 + b / 8, so the n/128 column tiles of a row band are computed at the same time on
 // ONE XCD and share the A rows through its L2.  G is a multiple of n/128, so a block always owns
-// the same column tile: its bias-gradient column sums stay in registers over all its tiles.
+// the same column tile: its bias-gradient column sums stay in registers over all its tiles.  The
+// epilogue goes through LDS so that global stores (and, backward, the y loads) are 16 B per lane.
 namespace vgemm {
 
-#ifndef VSS_LT_EPI
-#define VSS_LT_EPI 0
-#endif
 #ifndef VSS_LT_PERSIST
 #define VSS_LT_PERSIST 1
 #endif
@@ -174,6 +172,8 @@ __device__ __forceinline__ float tanh_f32(float z) {
 constexpr int kBM = 128, kBN = 128, kKS = 32, kLS = kKS + 4, kThreadsG = 256;
 constexpr int kTM = kBM / 64, kTN = kBN / 64;  // 32 x 32 tiles per wave (waves as 2 x 2)
 constexpr int kLdsFloats = 2 * (kBM + kBN) * kLS;
+constexpr int kES = 72;  // epilogue scratch row stride (floats): 4 waves x 32 x kES fit one K-tile buffer
+static_assert(4 * 32 * kES <= (kBM + kBN) * kLS, "epilogue scratch must fit one LDS buffer");
 constexpr int kBlocksPerCu = 2;  // 2 blocks per CU fit the LDS (72 KB each): 2 waves per SIMD
 constexpr int kRA = kBM * kKS / 4 / kThreadsG, kRB = kBN * kKS / 4 / kThreadsG;  // float4 staged per thread
 
@@ -196,51 +196,58 @@ __global__ __launch_bounds__(kThreadsG, kBlocksPerCu) void gemm_kernel(GemmArgs 
   const int nb = p.n / kBN;
   const int K = p.k, ktiles = (K + kKS - 1) / kKS;
   const int64_t M = p.rows;
-  const int G = gridDim.x;
-  const int64_t slot = (G % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : (int64_t)blockIdx.x;
-  if (slot >= p.tiles) return;  // whole block (the host sizes G <= tiles)
-  int64_t tile = slot;
+  const int G = gridDim.x, tiles = (int)p.tiles;
+  const int slot = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  if (slot >= tiles) return;  // whole block (the host sizes G <= tiles)
+  int tile = slot;
 
-  f32x16 acc[kTM][kTN];
-  float csum[kTN] = {0.0f, 0.0f};  // EPI_DTANH: this lane's column sums over all its tiles
+  // loader: thread tid stages rows lr + 32 i (i < kRA of A, < kRB of B) and floats lc..lc+3 of each K tile
+  const int lr = tid >> 3, lc = (tid & 7) * 4;
+  const int64_t K32 = (int64_t)32 * K;
+  const float* pa;  // this thread's first A row of the tile being fetched, at column lc
+  const float* pb;
+  int arows;        // rows of that tile below M
+  auto set_fetch_tile = [&](int t) {
+    const int64_t row0 = (int64_t)(t / nb) * kBM;
+    const int col0 = (t % nb) * kBN;
+    pa = p.a + (row0 + lr) * K + lc;
+    pb = p.b + (int64_t)(col0 + lr) * K + lc;
+    arows = (int)((M - row0) < kBM ? (M - row0) : kBM);
+  };
   float4 ra[kRA], rb[kRB];
-  auto gload = [&](int64_t t, int kt) {
-    const int64_t row0 = (t / nb) * kBM;
-    const int col0 = (int)(t % nb) * kBN;
+  auto gload = [&](int kt) {
+    const bool kin = kt * kKS + lc < K;
+    const int ko = kt * kKS;
 #pragma unroll
-    for (int i = 0; i < kRA; ++i) {
-      const int idx = tid + i * kThreadsG, r = idx >> 3, c = (idx & 7) * 4, kk = kt * kKS + c;
-      const int64_t gr = row0 + r;
-      ra[i] = (gr < M && kk < K) ? *reinterpret_cast<const float4*>(p.a + gr * K + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    for (int i = 0; i < kRA; ++i)
+      ra[i] = (kin && lr + 32 * i < arows) ? *reinterpret_cast<const float4*>(pa + i * K32 + ko) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int i = 0; i < kRB; ++i) {
-      const int idx = tid + i * kThreadsG, r = idx >> 3, c = (idx & 7) * 4, kk = kt * kKS + c;
-      rb[i] = kk < K ? *reinterpret_cast<const float4*>(p.b + (int64_t)(col0 + r) * K + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    for (int i = 0; i < kRB; ++i)
+      rb[i] = kin ? *reinterpret_cast<const float4*>(pb + i * K32 + ko) : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   auto swrite = [&](int buf) {
     float* As = lds + buf * (kBM + kBN) * kLS;
     float* Bs = As + kBM * kLS;
 #pragma unroll
-    for (int i = 0; i < kRA; ++i) {
-      const int idx = tid + i * kThreadsG;
-      *reinterpret_cast<float4*>(As + (idx >> 3) * kLS + (idx & 7) * 4) = ra[i];
-    }
+    for (int i = 0; i < kRA; ++i) *reinterpret_cast<float4*>(As + (lr + 32 * i) * kLS + lc) = ra[i];
 #pragma unroll
-    for (int i = 0; i < kRB; ++i) {
-      const int idx = tid + i * kThreadsG;
-      *reinterpret_cast<float4*>(Bs + (idx >> 3) * kLS + (idx & 7) * 4) = rb[i];
-    }
+    for (int i = 0; i < kRB; ++i) *reinterpret_cast<float4*>(Bs + (lr + 32 * i) * kLS + lc) = rb[i];
   };
 
-  gload(tile, 0);
+  f32x16 acc[kTM][kTN];
+  float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);  // EPI_DTANH: this lane's 4 column sums over all its tiles
+  set_fetch_tile(tile);
+  gload(0);
   swrite(0);
   __syncthreads();
   const int r = lane & 31, h = lane >> 5;
+  const int er = lane >> 4, ec = (lane & 15) * 4;  // epilogue reader: rows er + 4q, columns ec..ec+3
   int buf = 0;
   for (;;) {
-    const int64_t next = tile + G;
+    const int next = tile + G;
+    const bool has_next = next < tiles;
+    const int64_t row0 = (int64_t)(tile / nb) * kBM;
+    const int col0 = (tile % nb) * kBN;
 #pragma unroll
     for (int i = 0; i < kTM; ++i)
 #pragma unroll
@@ -248,9 +255,14 @@ __global__ __launch_bounds__(kThreadsG, kBlocksPerCu) void gemm_kernel(GemmArgs 
         acc[i][j] = (f32x16){0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int kt = 0; kt < ktiles; ++kt) {
       // the next K tile of the flat pipeline: this tile's kt + 1, else the next tile's first
-      const bool more = kt + 1 < ktiles || next < p.tiles;
-      if (kt + 1 < ktiles) gload(tile, kt + 1);
-      else if (more) gload(next, 0);
+      const bool last = kt + 1 == ktiles;
+      const bool more = !last || has_next;
+      if (!last) {
+        gload(kt + 1);
+      } else if (has_next) {
+        set_fetch_tile(next);
+        gload(0);
+      }
       const float* As = lds + buf * (kBM + kBN) * kLS + (wm * (kBM / 2) + r) * kLS + h * 16;
       const float* Bs = lds + buf * (kBM + kBN) * kLS + kBM * kLS + (wn * (kBN / 2) + r) * kLS + h * 16;
 #pragma unroll
@@ -278,54 +290,71 @@ __global__ __launch_bounds__(kThreadsG, kBlocksPerCu) void gemm_kernel(GemmArgs 
       }
     }
 
-    // epilogue, C/D map of the 32x32 tile: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
-    const int64_t row0 = (tile / nb) * kBM;
-    const int col0 = (int)(tile % nb) * kBN;
+    // Epilogue through the free LDS buffer (buf ^ 1: every wave has passed the barrier after its
+    // last read), one 32 x 64 half-tile per wave at a time, so that every global access is a 16-B
+    // piece of a 256-B row segment.  C/D map of a 32x32 tile: col = lane & 31,
+    // row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5).  Row stride kES = 72 floats: the two row halves
+    // of a ds_write_b32 land 32 banks apart, and each 16-lane ds_read_b128 group reads 64
+    // consecutive dwords (conflict-free both ways).
+    float* scr = lds + (buf ^ 1) * (kBM + kBN) * kLS + wv * (32 * kES);
+    const int colw = col0 + wn * (kBN / 2);
 #pragma unroll
-    for (int j = 0; j < kTN; ++j) {
-      const int col = col0 + wn * (kBN / 2) + j * 32 + r;
-      const float bcol = EPI == EPI_TANH ? p.bias[col] : 0.0f;
+    for (int i = 0; i < kTM; ++i) {
+      const int64_t rowb = row0 + wm * (kBM / 2) + i * 32;
+      float4 yv[8];
+      if constexpr (EPI == EPI_DTANH) {
 #pragma unroll
-      for (int i = 0; i < kTM; ++i) {
-        const int64_t rbase = row0 + wm * (kBM / 2) + i * 32 + 4 * h;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int64_t row = rbase + (e & 3) + 8 * (e >> 2);
-          if (row < M) {
-            const int64_t o = row * p.n + col;
-            if constexpr (EPI == EPI_TANH) {
-#if VSS_LT_EPI == 2  // profiling knob: no epilogue (one store per tile keeps the MFMAs live)
-              if (e == 0) p.out[o] = acc[i][j][0] + acc[i][j][5] + acc[i][j][15] + bcol;
-#elif VSS_LT_EPI == 1  // profiling knob: bias only
-              p.out[o] = acc[i][j][e] + bcol;
-#else
-              p.out[o] = tanh_f32(acc[i][j][e] + bcol);
-#endif
-            } else {
-              const float yv = p.y[o];
-              const float g = acc[i][j][e] * fmaf(-yv, yv, 1.0f);
-              p.out[o] = g;
-              csum[j] += g;
-            }
-          }
+        for (int q = 0; q < 8; ++q) {
+          const int64_t row = rowb + er + 4 * q;
+          yv[q] = row < M ? *reinterpret_cast<const float4*>(p.y + row * p.n + colw + ec) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
+#pragma unroll
+      for (int j = 0; j < kTN; ++j) {
+        const float bcol = EPI == EPI_TANH ? p.bias[colw + j * 32 + r] : 0.0f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          float v = acc[i][j][e];
+          if constexpr (EPI == EPI_TANH) v = tanh_f32(v + bcol);
+          scr[((e & 3) + 8 * (e >> 2) + 4 * h) * kES + j * 32 + r] = v;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float4 v = *reinterpret_cast<const float4*>(scr + (er + 4 * q) * kES + ec);
+        const int64_t row = rowb + er + 4 * q;
+        if constexpr (EPI == EPI_DTANH) {
+          const float4 yq = yv[q];
+          v = make_float4(v.x * fmaf(-yq.x, yq.x, 1.0f), v.y * fmaf(-yq.y, yq.y, 1.0f), v.z * fmaf(-yq.z, yq.z, 1.0f),
+                          v.w * fmaf(-yq.w, yq.w, 1.0f));
+          if (row < M) vupd::add4(csum, v);
+        }
+        if (row < M) *reinterpret_cast<float4*>(p.out + row * p.n + colw + ec) = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (next >= p.tiles) break;
+    if (!has_next) break;
+    __syncthreads();  // the next tile's first swrite reuses the scratch buffer
     tile = next;
   }
 
   if constexpr (EPI == EPI_DTANH) {
-    // the block's column sums: lane halves (rows 4h..), then the two row waves (wm), fixed order
-    __syncthreads();  // every wave is done with the pipeline's LDS buffers
+    // the block's column sums: the 4 row groups of a wave (lanes ec/4, +16, +32, +48), then the two
+    // row waves (wm), in a fixed order
+    csum.x += __shfl_xor(csum.x, 16); csum.y += __shfl_xor(csum.y, 16);
+    csum.z += __shfl_xor(csum.z, 16); csum.w += __shfl_xor(csum.w, 16);
+    csum.x += __shfl_xor(csum.x, 32); csum.y += __shfl_xor(csum.y, 32);
+    csum.z += __shfl_xor(csum.z, 32); csum.w += __shfl_xor(csum.w, 32);
+    __syncthreads();  // every wave is done with the LDS buffers
     float* red = lds;  // [2][kBN]
-#pragma unroll
-    for (int j = 0; j < kTN; ++j) {
-      const float v = csum[j] + __shfl_xor(csum[j], 32);
-      if (h == 0) red[wm * kBN + wn * (kBN / 2) + j * 32 + r] = v;
-    }
+    if (er == 0) *reinterpret_cast<float4*>(red + wm * kBN + wn * (kBN / 2) + ec) = csum;
     __syncthreads();
-    if (tid < kBN) p.partial[(slot / nb) * p.n + (slot % nb) * kBN + tid] = red[tid] + red[kBN + tid];
+    if (tid < kBN) p.partial[(int64_t)(slot / nb) * p.n + (slot % nb) * kBN + tid] = red[tid] + red[kBN + tid];
   }
 }
 
@@ -358,7 +387,7 @@ static int64_t grid_for(int64_t tiles, int nb) {
 
 static bool shape_ok(int64_t rows, int32_t k, int32_t n) {
   return rows >= 0 && rows <= (int64_t(1) << 40) && k >= 4 && k % 4 == 0 && k <= 65536 && n >= kBN && n % kBN == 0 &&
-         n <= 65536 && (rows + kBM - 1) / kBM * (n / kBN) <= 0x7fffffff;
+         n <= 65536 && (rows + kBM - 1) / kBM * (n / kBN) <= 0x7fff0000;  // tile + grid stays in int
 }
 
 static int64_t tiles_for(int64_t rows, int32_t n) { return (rows + kBM - 1) / kBM * (n / kBN); }

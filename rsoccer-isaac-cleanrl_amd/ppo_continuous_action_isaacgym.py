@@ -226,12 +226,11 @@ class _TanhMLP(torch.autograd.Function):
         return (gx, *grads)
 
 
-# the update's MLP path: "split" (default) = _LinearTanh / _LinearSplitK (hipBLASLt GEMMs + the
-# one-pass HIP tanh backward); "fused" = _TanhMLP (our fp32 MFMA GEMMs with the tanh work in their
-# epilogues).  "fused" saves the elementwise passes but its GEMM body runs at 83-117 TF against
-# hipBLASLt's 133-144 TF on these shapes, so it is slower end to end (DESIGN.md §5.3,
-# profiles/r01_gemm_fused_bench.log); opt in with VSS_UPDATE_MLP=fused.
-UPDATE_MLP = os.environ.get("VSS_UPDATE_MLP", "split")
+# the update's MLP path: "fused" (default) = _TanhMLP (our fp32 MFMA GEMMs with the tanh work in
+# their epilogues: 3.80 s per SA update at 65,536 envs); "split" = _LinearTanh / _LinearSplitK
+# (hipBLASLt GEMMs + the one-pass HIP tanh backward: 3.99 s).  DESIGN.md §5.3,
+# profiles/r01_gemm_fused_bench.log, profiles/r01_ppo_update_fused_vs_split.log.
+UPDATE_MLP = os.environ.get("VSS_UPDATE_MLP", "fused")
 
 
 def _fused_mlp_ok(seq: nn.Sequential) -> bool:

@@ -149,6 +149,9 @@ namespace vgemm {
 #ifndef VSS_LT_PERSIST
 #define VSS_LT_PERSIST 1
 #endif
+#ifndef VSS_LT_PROBE
+#define VSS_LT_PROBE 0
+#endif
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 enum { EPI_TANH = 0, EPI_DTANH = 1 };
@@ -169,13 +172,26 @@ __device__ __forceinline__ float tanh_f32(float z) {
 #endif
 }
 
-constexpr int kBM = 128, kBN = 128, kKS = 32, kLS = kKS + 4, kThreadsG = 256;
-constexpr int kTM = kBM / 64, kTN = kBN / 64;  // 32 x 32 tiles per wave (waves as 2 x 2)
-constexpr int kLdsFloats = 2 * (kBM + kBN) * kLS;
-constexpr int kES = 72;  // epilogue scratch row stride (floats): 4 waves x 32 x kES fit one K-tile buffer
-static_assert(4 * 32 * kES <= (kBM + kBN) * kLS, "epilogue scratch must fit one LDS buffer");
-constexpr int kBlocksPerCu = 2;  // 2 blocks per CU fit the LDS (72 KB each): 2 waves per SIMD
-constexpr int kRA = kBM * kKS / 4 / kThreadsG, kRB = kBN * kKS / 4 / kThreadsG;  // float4 staged per thread
+constexpr int kKS = 32, kLS = kKS + 4;  // K tile, LDS row stride (floats; conflict-free ds_read_b128 groups)
+constexpr int kES = 72;  // epilogue scratch row stride (floats)
+
+// Block geometry: BM x BN output tile, WM x WN waves, each a (BM/WM) x (BN/WN) block of 32x32 MFMA tiles.
+template <int BM_, int BN_, int WM_, int WN_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_;
+  static constexpr int THREADS = 64 * WM * WN;
+  static constexpr int WROWS = BM / WM, WCOLS = BN / WN;
+  static constexpr int TM = WROWS / 32, TN = WCOLS / 32;
+  static constexpr int LDSF = 2 * (BM + BN) * kLS;  // two K-tile buffers
+  static constexpr int LROWS = THREADS / 8;          // rows one staging pass covers (8 float4 per 32-float row)
+  static constexpr int RA = BM / LROWS, RB = BN / LROWS;
+  static constexpr int BLOCKS_PER_CU = LDSF * 4 * 2 <= 160 * 1024 ? 2 : 1;
+  static_assert(WCOLS == 64, "the epilogue streams 64-column wave tiles");
+  static_assert(WM * WN * 32 * kES <= (BM + BN) * kLS, "epilogue scratch must fit one K-tile buffer");
+  static_assert(RA * LROWS == BM && RB * LROWS == BN, "staging passes must tile the block");
+};
+using Cfg128 = Cfg<128, 128, 2, 2>;  // 4 waves, 72 KB LDS: two blocks per CU
+using Cfg256 = Cfg<256, 256, 2, 4>;  // 8 waves of 128 x 64, 144 KB LDS: one block per CU
 
 struct GemmArgs {
   int64_t rows;
@@ -185,15 +201,95 @@ struct GemmArgs {
   const float* bias;  // EPI_TANH: (n)
   const float* y;     // EPI_DTANH: (rows, n), the tanh output the gradient passes through
   float* out;         // (rows, n)
-  float* partial;     // EPI_DTANH: (G / (n / kBN), n) column sums of out
-  int64_t tiles;      // ceil(rows / kBM) * (n / kBN) output tiles, row band major
+  float* partial;     // EPI_DTANH: (G / (n / BN), n) column sums of out
+  int64_t tiles;      // ceil(rows / BM) * (n / BN) output tiles, row band major
 };
 
-template <int EPI>
-__global__ __launch_bounds__(kThreadsG, kBlocksPerCu) void gemm_kernel(GemmArgs p) {
-  __shared__ float lds[kLdsFloats];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
-  const int nb = p.n / kBN;
+// One wave's (TM x 32) x 64 output block, 32 x 64 at a time through the wave's LDS scratch (32 x kES
+// floats), so that every global access is a 16-B piece of a 256-B row segment.  C/D map of a 32x32
+// MFMA tile: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5).  Row stride kES = 72: the
+// two row halves of a ds_write_b32 land 32 banks apart and each 16-lane ds_read_b128 group reads 64
+// consecutive dwords (conflict-free both ways).  EPI_TANH: out = tanh(acc + bias); EPI_DTANH:
+// out = acc * (1 - y^2) and csum += out (this lane's 4 columns).
+template <int EPI, int TM, int TN>
+__device__ __forceinline__ void store_tile(const GemmArgs& p, f32x16 (&acc)[TM][TN], float* scr, int64_t rowb0, int colw,
+                                           float4& csum) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int er = lane >> 4, ec = (lane & 15) * 4;  // reader: rows er + 4q, columns ec..ec+3
+  const int64_t M = p.rows;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int64_t rowb = rowb0 + i * 32;
+    // EPI_DTANH: y of rows er + 4q, four rows in flight (loaded before the LDS round trip, then each
+    // slot refilled with the row four steps ahead as it is consumed)
+    auto yload = [&](int q) {
+      const int64_t row = rowb + er + 4 * q;
+      return row < M ? *reinterpret_cast<const float4*>(p.y + row * p.n + colw + ec) : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    float4 yv[4];
+    if constexpr (EPI == EPI_DTANH) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) yv[q] = yload(q);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float bcol = EPI == EPI_TANH ? p.bias[colw + j * 32 + r] : 0.0f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        float v = acc[i][j][e];
+        if constexpr (EPI == EPI_TANH) v = tanh_f32(v + bcol);
+        scr[((e & 3) + 8 * (e >> 2) + 4 * h) * kES + j * 32 + r] = v;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float4 v = *reinterpret_cast<const float4*>(scr + (er + 4 * q) * kES + ec);
+      const int64_t row = rowb + er + 4 * q;
+      if constexpr (EPI == EPI_DTANH) {
+        const float4 yq = yv[q & 3];
+        if (q < 4) yv[q] = yload(q + 4);
+        v = make_float4(v.x * fmaf(-yq.x, yq.x, 1.0f), v.y * fmaf(-yq.y, yq.y, 1.0f), v.z * fmaf(-yq.z, yq.z, 1.0f),
+                        v.w * fmaf(-yq.w, yq.w, 1.0f));
+        if (row < M) vupd::add4(csum, v);
+      }
+      if (row < M) *reinterpret_cast<float4*>(p.out + row * p.n + colw + ec) = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// EPI_DTANH: the block's column sums into partial row slot / nb — the 4 row groups of a wave (lanes
+// ec/4, +16, +32, +48), then the WM row waves, in a fixed order (deterministic).  `red` is LDS the
+// caller has released (a __syncthreads() before the call).
+template <int WM, int BN>
+__device__ __forceinline__ void write_colsums(const GemmArgs& p, float4 csum, float* red, int slot, int nb, int wm,
+                                              int wcol) {
+  const int tid = threadIdx.x, lane = tid & 63, er = lane >> 4, ec = (lane & 15) * 4;
+  csum.x += __shfl_xor(csum.x, 16); csum.y += __shfl_xor(csum.y, 16);
+  csum.z += __shfl_xor(csum.z, 16); csum.w += __shfl_xor(csum.w, 16);
+  csum.x += __shfl_xor(csum.x, 32); csum.y += __shfl_xor(csum.y, 32);
+  csum.z += __shfl_xor(csum.z, 32); csum.w += __shfl_xor(csum.w, 32);
+  if (er == 0) *reinterpret_cast<float4*>(red + wm * BN + wcol + ec) = csum;
+  __syncthreads();
+  if (tid < BN) {
+    float s = red[tid];
+#pragma unroll
+    for (int m = 1; m < WM; ++m) s += red[m * BN + tid];
+    p.partial[(int64_t)(slot / nb) * p.n + (slot % nb) * BN + tid] = s;
+  }
+}
+
+template <int EPI, class C>
+__global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(GemmArgs p) {
+  constexpr int BM = C::BM, BN = C::BN, TM = C::TM, TN = C::TN, LROWS = C::LROWS;
+  __shared__ float lds[C::LDSF];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv / C::WN, wn = wv % C::WN;
+  const int nb = p.n / BN;
   const int K = p.k, ktiles = (K + kKS - 1) / kKS;
   const int64_t M = p.rows;
   const int G = gridDim.x, tiles = (int)p.tiles;
@@ -201,57 +297,60 @@ __global__ __launch_bounds__(kThreadsG, kBlocksPerCu) void gemm_kernel(GemmArgs 
   if (slot >= tiles) return;  // whole block (the host sizes G <= tiles)
   int tile = slot;
 
-  // loader: thread tid stages rows lr + 32 i (i < kRA of A, < kRB of B) and floats lc..lc+3 of each K tile
+  // loader: thread tid stages rows lr + LROWS i and floats lc..lc+3 of each K tile
   const int lr = tid >> 3, lc = (tid & 7) * 4;
-  const int64_t K32 = (int64_t)32 * K;
+  const int64_t KL = (int64_t)LROWS * K;
   const float* pa;  // this thread's first A row of the tile being fetched, at column lc
   const float* pb;
   int arows;        // rows of that tile below M
   auto set_fetch_tile = [&](int t) {
-    const int64_t row0 = (int64_t)(t / nb) * kBM;
-    const int col0 = (t % nb) * kBN;
+    const int64_t row0 = (int64_t)(t / nb) * BM;
+    const int col0 = (t % nb) * BN;
     pa = p.a + (row0 + lr) * K + lc;
     pb = p.b + (int64_t)(col0 + lr) * K + lc;
-    arows = (int)((M - row0) < kBM ? (M - row0) : kBM);
+    arows = (int)((M - row0) < BM ? (M - row0) : BM);
   };
-  float4 ra[kRA], rb[kRB];
+  float4 ra[C::RA], rb[C::RB];
+  // Conditional loads (zero outside the matrix).  Measured: loading unconditionally from clamped
+  // addresses and applying the validity only when the staged registers are written to LDS (so that
+  // the compiler does not wait for the loads before this K tile's MFMAs) ran 10 % SLOWER
+  // (profiles/r01_gemm_fused_bench.log notes).
   auto gload = [&](int kt) {
     const bool kin = kt * kKS + lc < K;
     const int ko = kt * kKS;
 #pragma unroll
-    for (int i = 0; i < kRA; ++i)
-      ra[i] = (kin && lr + 32 * i < arows) ? *reinterpret_cast<const float4*>(pa + i * K32 + ko) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < C::RA; ++i)
+      ra[i] = (kin && lr + LROWS * i < arows) ? *reinterpret_cast<const float4*>(pa + i * KL + ko) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int i = 0; i < kRB; ++i)
-      rb[i] = kin ? *reinterpret_cast<const float4*>(pb + i * K32 + ko) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < C::RB; ++i)
+      rb[i] = kin ? *reinterpret_cast<const float4*>(pb + i * KL + ko) : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   auto swrite = [&](int buf) {
-    float* As = lds + buf * (kBM + kBN) * kLS;
-    float* Bs = As + kBM * kLS;
+    float* As = lds + buf * (BM + BN) * kLS;
+    float* Bs = As + BM * kLS;
 #pragma unroll
-    for (int i = 0; i < kRA; ++i) *reinterpret_cast<float4*>(As + (lr + 32 * i) * kLS + lc) = ra[i];
+    for (int i = 0; i < C::RA; ++i) *reinterpret_cast<float4*>(As + (lr + LROWS * i) * kLS + lc) = ra[i];
 #pragma unroll
-    for (int i = 0; i < kRB; ++i) *reinterpret_cast<float4*>(Bs + (lr + 32 * i) * kLS + lc) = rb[i];
+    for (int i = 0; i < C::RB; ++i) *reinterpret_cast<float4*>(Bs + (lr + LROWS * i) * kLS + lc) = rb[i];
   };
 
-  f32x16 acc[kTM][kTN];
+  f32x16 acc[TM][TN];
   float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);  // EPI_DTANH: this lane's 4 column sums over all its tiles
   set_fetch_tile(tile);
   gload(0);
   swrite(0);
   __syncthreads();
   const int r = lane & 31, h = lane >> 5;
-  const int er = lane >> 4, ec = (lane & 15) * 4;  // epilogue reader: rows er + 4q, columns ec..ec+3
   int buf = 0;
   for (;;) {
     const int next = tile + G;
     const bool has_next = next < tiles;
-    const int64_t row0 = (int64_t)(tile / nb) * kBM;
-    const int col0 = (tile % nb) * kBN;
+    const int64_t row0 = (int64_t)(tile / nb) * BM;
+    const int col0 = (tile % nb) * BN;
 #pragma unroll
-    for (int i = 0; i < kTM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < kTN; ++j)
+      for (int j = 0; j < TN; ++j)
         acc[i][j] = (f32x16){0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int kt = 0; kt < ktiles; ++kt) {
       // the next K tile of the flat pipeline: this tile's kt + 1, else the next tile's first
@@ -263,134 +362,110 @@ __global__ __launch_bounds__(kThreadsG, kBlocksPerCu) void gemm_kernel(GemmArgs 
         set_fetch_tile(next);
         gload(0);
       }
-      const float* As = lds + buf * (kBM + kBN) * kLS + (wm * (kBM / 2) + r) * kLS + h * 16;
-      const float* Bs = lds + buf * (kBM + kBN) * kLS + kBM * kLS + (wn * (kBN / 2) + r) * kLS + h * 16;
+      const float* As = lds + buf * (BM + BN) * kLS + (wm * C::WROWS + r) * kLS + h * 16;
+      const float* Bs = lds + buf * (BM + BN) * kLS + BM * kLS + (wn * C::WCOLS + r) * kLS + h * 16;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        float4 a4[kTM], b4[kTN];
+        float4 a4[TM], b4[TN];
+#if VSS_LT_PROBE == 1  // profiling knob: operands from registers only (no LDS reads in the K loop)
 #pragma unroll
-        for (int i = 0; i < kTM; ++i) a4[i] = *reinterpret_cast<const float4*>(As + i * 32 * kLS + q * 4);
+        for (int i = 0; i < TM; ++i) a4[i] = ra[i % C::RA];
 #pragma unroll
-        for (int j = 0; j < kTN; ++j) b4[j] = *reinterpret_cast<const float4*>(Bs + j * 32 * kLS + q * 4);
+        for (int j = 0; j < TN; ++j) b4[j] = rb[j % C::RB];
+#else
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a4[i] = *reinterpret_cast<const float4*>(As + i * 32 * kLS + q * 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b4[j] = *reinterpret_cast<const float4*>(Bs + j * 32 * kLS + q * 4);
+#endif
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
-          for (int i = 0; i < kTM; ++i)
+          for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < kTN; ++j) {
+            for (int j = 0; j < TN; ++j) {
               const float av = s == 0 ? a4[i].x : s == 1 ? a4[i].y : s == 2 ? a4[i].z : a4[i].w;
               const float bv = s == 0 ? b4[j].x : s == 1 ? b4[j].y : s == 2 ? b4[j].z : b4[j].w;
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
             }
       }
+#if VSS_LT_PROBE != 2  // profiling knob 2: no LDS staging / barrier (wrong results, timing only)
       if (more) {
         swrite(buf ^ 1);
         __syncthreads();
         buf ^= 1;
       }
+#endif
     }
 
-    // Epilogue through the free LDS buffer (buf ^ 1: every wave has passed the barrier after its
-    // last read), one 32 x 64 half-tile per wave at a time, so that every global access is a 16-B
-    // piece of a 256-B row segment.  C/D map of a 32x32 tile: col = lane & 31,
-    // row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5).  Row stride kES = 72 floats: the two row halves
-    // of a ds_write_b32 land 32 banks apart, and each 16-lane ds_read_b128 group reads 64
-    // consecutive dwords (conflict-free both ways).
-    float* scr = lds + (buf ^ 1) * (kBM + kBN) * kLS + wv * (32 * kES);
-    const int colw = col0 + wn * (kBN / 2);
-#pragma unroll
-    for (int i = 0; i < kTM; ++i) {
-      const int64_t rowb = row0 + wm * (kBM / 2) + i * 32;
-      float4 yv[8];
-      if constexpr (EPI == EPI_DTANH) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int64_t row = rowb + er + 4 * q;
-          yv[q] = row < M ? *reinterpret_cast<const float4*>(p.y + row * p.n + colw + ec) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < kTN; ++j) {
-        const float bcol = EPI == EPI_TANH ? p.bias[colw + j * 32 + r] : 0.0f;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          float v = acc[i][j][e];
-          if constexpr (EPI == EPI_TANH) v = tanh_f32(v + bcol);
-          scr[((e & 3) + 8 * (e >> 2) + 4 * h) * kES + j * 32 + r] = v;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float4 v = *reinterpret_cast<const float4*>(scr + (er + 4 * q) * kES + ec);
-        const int64_t row = rowb + er + 4 * q;
-        if constexpr (EPI == EPI_DTANH) {
-          const float4 yq = yv[q];
-          v = make_float4(v.x * fmaf(-yq.x, yq.x, 1.0f), v.y * fmaf(-yq.y, yq.y, 1.0f), v.z * fmaf(-yq.z, yq.z, 1.0f),
-                          v.w * fmaf(-yq.w, yq.w, 1.0f));
-          if (row < M) vupd::add4(csum, v);
-        }
-        if (row < M) *reinterpret_cast<float4*>(p.out + row * p.n + colw + ec) = v;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
+    // epilogue through the free LDS buffer (buf ^ 1: every wave has passed the barrier after its last read)
+    store_tile<EPI, TM, TN>(p, acc, lds + (buf ^ 1) * (BM + BN) * kLS + wv * (32 * kES), row0 + wm * C::WROWS,
+                            col0 + wn * C::WCOLS, csum);
     if (!has_next) break;
     __syncthreads();  // the next tile's first swrite reuses the scratch buffer
     tile = next;
   }
 
   if constexpr (EPI == EPI_DTANH) {
-    // the block's column sums: the 4 row groups of a wave (lanes ec/4, +16, +32, +48), then the two
-    // row waves (wm), in a fixed order
-    csum.x += __shfl_xor(csum.x, 16); csum.y += __shfl_xor(csum.y, 16);
-    csum.z += __shfl_xor(csum.z, 16); csum.w += __shfl_xor(csum.w, 16);
-    csum.x += __shfl_xor(csum.x, 32); csum.y += __shfl_xor(csum.y, 32);
-    csum.z += __shfl_xor(csum.z, 32); csum.w += __shfl_xor(csum.w, 32);
     __syncthreads();  // every wave is done with the LDS buffers
-    float* red = lds;  // [2][kBN]
-    if (er == 0) *reinterpret_cast<float4*>(red + wm * kBN + wn * (kBN / 2) + ec) = csum;
-    __syncthreads();
-    if (tid < kBN) p.partial[(int64_t)(slot / nb) * p.n + (slot % nb) * kBN + tid] = red[tid] + red[kBN + tid];
+    write_colsums<C::WM, BN>(p, csum, lds, slot, nb, wm, wn * C::WCOLS);
   }
 }
 
-// CUs of the current device (cached per device; an attribute query, no synchronisation)
-static int n_cus() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  if (cached[dev] <= 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cached[dev] = n;
-  }
-  return cached[dev];
-}
+// The persistent grid is sized for MI355X (256 CUs) on every device: a block walks its tiles however
+// many blocks are resident, so the grid -- and with it the bias-gradient partial layout and its
+// summation order -- does not depend on the device the call runs on.
+constexpr int kGridCus = 256;
 
-// grid: min(tiles, blocks_per_cu x CUs), the latter rounded down to a multiple of 8 (XCD slots) and
-// of n / kBN (a fixed column tile per block)
-static int64_t grid_for(int64_t tiles, int nb) {
-#if VSS_LT_PERSIST
-  int64_t g = (int64_t)n_cus() * kBlocksPerCu;
-  const int64_t q = 8 * (int64_t)nb;
-  g -= g % q;
-  if (g > 0 && g < tiles) return g;
-#else
-  (void)nb;
+#ifndef VSS_LT_CFG
+#define VSS_LT_CFG 256  // 256: 256 x 256 blocks where n % 256 == 0 (else 128 x 128); 128: always 128 x 128
 #endif
-  return tiles;
+
+// the launch plan of one GEMM: kernel, output tiles, grid
+struct Plan {
+  int kind;  // 0 Cfg128, 1 Cfg256
+  int bn;
+  int64_t tiles, grid;
+};
+
+static Plan plan(int64_t rows, int32_t n) {
+  Plan pl;
+  pl.kind = (VSS_LT_CFG == 256 && n % 256 == 0) ? 1 : 0;
+  static const int BMs[2] = {Cfg128::BM, Cfg256::BM};
+  static const int BNs[2] = {Cfg128::BN, Cfg256::BN};
+  static const int BPC[2] = {Cfg128::BLOCKS_PER_CU, Cfg256::BLOCKS_PER_CU};
+  const int bm = BMs[pl.kind];
+  pl.bn = BNs[pl.kind];
+  const int nb = n / pl.bn;
+  pl.tiles = (rows + bm - 1) / bm * nb;
+  pl.grid = pl.tiles;
+#if VSS_LT_PERSIST
+  // min(tiles, blocks_per_cu x CUs), the latter rounded down to a multiple of 8 (XCD slots) and of
+  // nb (a fixed column tile per block)
+  int64_t g = (int64_t)kGridCus * BPC[pl.kind];
+  g -= g % (8 * (int64_t)nb);
+  if (g > 0 && g < pl.tiles) pl.grid = g;
+#endif
+  return pl;
 }
 
 static bool shape_ok(int64_t rows, int32_t k, int32_t n) {
-  return rows >= 0 && rows <= (int64_t(1) << 40) && k >= 4 && k % 4 == 0 && k <= 65536 && n >= kBN && n % kBN == 0 &&
-         n <= 65536 && (rows + kBM - 1) / kBM * (n / kBN) <= 0x7fff0000;  // tile + grid stays in int
+  return rows >= 0 && rows <= (int64_t(1) << 40) && k >= 4 && k % 4 == 0 && k <= 65536 && n >= 128 && n % 128 == 0 &&
+         n <= 65536 && (rows + 127) / 128 * (n / 128) <= 0x7fff0000;  // tile + grid stays in int
 }
 
-static int64_t tiles_for(int64_t rows, int32_t n) { return (rows + kBM - 1) / kBM * (n / kBN); }
+template <int EPI>
+static int launch(void* stream, const GemmArgs& a0, const Plan& pl) {
+  GemmArgs a = a0;
+  a.tiles = pl.tiles;
+  const dim3 grid((unsigned)pl.grid);
+  hipStream_t s = (hipStream_t)stream;
+  switch (pl.kind) {
+    case 1: hipLaunchKernelGGL((gemm_kernel<EPI, Cfg256>), grid, dim3(Cfg256::THREADS), 0, s, a); break;
+    default: hipLaunchKernelGGL((gemm_kernel<EPI, Cfg128>), grid, dim3(Cfg128::THREADS), 0, s, a); break;
+  }
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+}
 
 }  // namespace vgemm
 
@@ -434,19 +509,15 @@ int vss_linear_tanh(void* stream, int64_t rows, int32_t k_in, int32_t n_out, con
   if (!vgemm::shape_ok(rows, k_in, n_out) || misaligned(x) || misaligned(w) || misaligned(y) || !bias)
     return VSS_E_ARG;
   if (rows == 0) return VSS_OK;
-  const int64_t tiles = vgemm::tiles_for(rows, n_out);
-  vgemm::GemmArgs a{rows, n_out, k_in, x, w, bias, nullptr, y, nullptr, tiles};
-  const int64_t grid = vgemm::grid_for(tiles, n_out / vgemm::kBN);
-  hipLaunchKernelGGL(vgemm::gemm_kernel<vgemm::EPI_TANH>, dim3((unsigned)grid), dim3(vgemm::kThreadsG), 0,
-                     (hipStream_t)stream, a);
-  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+  const vgemm::GemmArgs a{rows, n_out, k_in, x, w, bias, nullptr, y, nullptr, 0};
+  return vgemm::launch<vgemm::EPI_TANH>(stream, a, vgemm::plan(rows, n_out));
 }
 
 int64_t vss_linear_tanh_backward_chunks(int64_t rows, int32_t k_next, int32_t n_out) {
   if (!vgemm::shape_ok(rows, k_next, n_out)) return -1;
   if (rows == 0) return 0;
-  const int nb = n_out / vgemm::kBN;
-  return vgemm::grid_for(vgemm::tiles_for(rows, n_out), nb) / nb;
+  const vgemm::Plan pl = vgemm::plan(rows, n_out);
+  return pl.grid / (n_out / pl.bn);
 }
 
 int vss_linear_tanh_backward(void* stream, int64_t rows, int32_t k_next, int32_t n_out, const float* grad_next,
@@ -455,12 +526,8 @@ int vss_linear_tanh_backward(void* stream, int64_t rows, int32_t k_next, int32_t
       misaligned(grad_in) || misaligned(bias_partial))
     return VSS_E_ARG;
   if (rows == 0) return VSS_OK;
-  const int64_t tiles = vgemm::tiles_for(rows, n_out);
-  vgemm::GemmArgs a{rows, n_out, k_next, grad_next, w_next_t, nullptr, y, grad_in, bias_partial, tiles};
-  const int64_t grid = vgemm::grid_for(tiles, n_out / vgemm::kBN);
-  hipLaunchKernelGGL(vgemm::gemm_kernel<vgemm::EPI_DTANH>, dim3((unsigned)grid), dim3(vgemm::kThreadsG), 0,
-                     (hipStream_t)stream, a);
-  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+  const vgemm::GemmArgs a{rows, n_out, k_next, grad_next, w_next_t, nullptr, y, grad_in, bias_partial, 0};
+  return vgemm::launch<vgemm::EPI_DTANH>(stream, a, vgemm::plan(rows, n_out));
 }
 
 }  // extern "C"

@@ -51,6 +51,10 @@ case ",$STEPS," in *,gemm,*)
   VSS_UPDATE_MLP=fused run ppo_fused 300 python -u rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 3 --log false
   VSS_UPDATE_MLP=split run ppo_split 300 python -u rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 3 --log false ;;
 esac
+case ",$STEPS," in *,sa1e8,*)
+  run ppo_sa_1e8 600 python -u rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 \
+      --total-timesteps 100663296 --save-path "$OUT/runs_$TAG" ;;
+esac
 case ",$STEPS," in *,tdist,*) run pytest_dist 600 python -m pytest tests/test_dist.py -m gpu -x -q ;; esac
 case ",$STEPS," in *,amp,*) run ppo_amp 900 python rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 2 --amp bf16 --save-path /tmp/runs ;; esac
 case ",$STEPS," in *,ppoprof,*)

@@ -152,6 +152,9 @@ namespace vgemm {
 #ifndef VSS_LT_PROBE
 #define VSS_LT_PROBE 0
 #endif
+#ifndef VSS_LT_EXACT
+#define VSS_LT_EXACT 1  // unmasked loads for exact shapes
+#endif
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 enum { EPI_TANH = 0, EPI_DTANH = 1 };
@@ -284,7 +287,7 @@ __device__ __forceinline__ void write_colsums(const GemmArgs& p, float4 csum, fl
   }
 }
 
-template <int EPI, class C>
+template <int EPI, class C, bool EXACT>
 __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(GemmArgs p) {
   constexpr int BM = C::BM, BN = C::BN, TM = C::TM, TN = C::TN, LROWS = C::LROWS;
   __shared__ float lds[C::LDSF];
@@ -310,22 +313,36 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(Gemm
     pb = p.b + (int64_t)(col0 + lr) * K + lc;
     arows = (int)((M - row0) < BM ? (M - row0) : BM);
   };
-  float4 ra[C::RA], rb[C::RB];
-  // Conditional loads (zero outside the matrix).  Measured: loading unconditionally from clamped
-  // addresses and applying the validity only when the staged registers are written to LDS (so that
-  // the compiler does not wait for the loads before this K tile's MFMAs) ran 10 % SLOWER
-  // (profiles/r01_gemm_fused_bench.log notes).
-  auto gload = [&](int kt) {
-    const bool kin = kt * kKS + lc < K;
+  // EXACT (rows % BM == 0 and K % 32 == 0, the update's shapes but the first layer): plain loads whose
+  // registers are first read by the LDS write at the end of the K tile, so they stay in flight
+  // during the MFMAs.  Otherwise the masked form below, after which the compiler waits for the
+  // loads before the MFMAs (measured: the global loads then cost ~11 %, a barrier-free probe ~7 %).
+  auto gload = [&](float4 (&ra)[C::RA], float4 (&rb)[C::RB], int kt) {
     const int ko = kt * kKS;
+    if constexpr (EXACT) {
+      // loaded as a vector value (a float4 struct copy became a memcpy into a private array that
+      // was not promoted to registers)
 #pragma unroll
-    for (int i = 0; i < C::RA; ++i)
-      ra[i] = (kin && lr + LROWS * i < arows) ? *reinterpret_cast<const float4*>(pa + i * KL + ko) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int i = 0; i < C::RA; ++i) {
+        const vupd::f32x4 v = *reinterpret_cast<const vupd::f32x4*>(pa + i * KL + ko);
+        ra[i] = make_float4(v.x, v.y, v.z, v.w);
+      }
 #pragma unroll
-    for (int i = 0; i < C::RB; ++i)
-      rb[i] = kin ? *reinterpret_cast<const float4*>(pb + i * KL + ko) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int i = 0; i < C::RB; ++i) {
+        const vupd::f32x4 v = *reinterpret_cast<const vupd::f32x4*>(pb + i * KL + ko);
+        rb[i] = make_float4(v.x, v.y, v.z, v.w);
+      }
+    } else {
+      const bool kin = kt * kKS + lc < K;
+#pragma unroll
+      for (int i = 0; i < C::RA; ++i)
+        ra[i] = (kin && lr + LROWS * i < arows) ? *reinterpret_cast<const float4*>(pa + i * KL + ko) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < C::RB; ++i)
+        rb[i] = kin ? *reinterpret_cast<const float4*>(pb + i * KL + ko) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   };
-  auto swrite = [&](int buf) {
+  auto swrite = [&](const float4 (&ra)[C::RA], const float4 (&rb)[C::RB], int buf) {
     float* As = lds + buf * (BM + BN) * kLS;
     float* Bs = As + BM * kLS;
 #pragma unroll
@@ -337,8 +354,11 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(Gemm
   f32x16 acc[TM][TN];
   float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);  // EPI_DTANH: this lane's 4 column sums over all its tiles
   set_fetch_tile(tile);
-  gload(0);
-  swrite(0);
+  {
+    float4 ra[C::RA], rb[C::RB];
+    gload(ra, rb, 0);
+    swrite(ra, rb, 0);
+  }
   __syncthreads();
   const int r = lane & 31, h = lane >> 5;
   int buf = 0;
@@ -353,15 +373,20 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(Gemm
       for (int j = 0; j < TN; ++j)
         acc[i][j] = (f32x16){0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int kt = 0; kt < ktiles; ++kt) {
+      float4 ra[C::RA], rb[C::RB];  // the next K tile's operands, staged through registers
       // the next K tile of the flat pipeline: this tile's kt + 1, else the next tile's first
       const bool last = kt + 1 == ktiles;
       const bool more = !last || has_next;
-      if (!last) {
-        gload(kt + 1);
-      } else if (has_next) {
-        set_fetch_tile(next);
-        gload(0);
-      }
+#if VSS_LT_PROBE == 4  // profiling knob 4: no global loads in the K loop (stale staging, timing only)
+      if (last && has_next) set_fetch_tile(next);
+#else
+      // one load site, no branch around it: the loaded registers then need no copies at a control
+      // flow join (copies made the compiler wait for the loads before the MFMAs).  After the
+      // block's last tile this re-fetches its first K tile, which is never written to LDS.
+      if (last && has_next) set_fetch_tile(next);
+      gload(ra, rb, last ? 0 : kt + 1);
+      __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMAs (the scheduler sinks them)
+#endif
       const float* As = lds + buf * (BM + BN) * kLS + (wm * C::WROWS + r) * kLS + h * 16;
       const float* Bs = lds + buf * (BM + BN) * kLS + BM * kLS + (wn * C::WCOLS + r) * kLS + h * 16;
 #pragma unroll
@@ -391,8 +416,10 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(Gemm
       }
 #if VSS_LT_PROBE != 2  // profiling knob 2: no LDS staging / barrier (wrong results, timing only)
       if (more) {
-        swrite(buf ^ 1);
+        swrite(ra, rb, buf ^ 1);
+#if VSS_LT_PROBE != 3  // profiling knob 3: no barrier (wrong results, timing only)
         __syncthreads();
+#endif
         buf ^= 1;
       }
 #endif
@@ -418,7 +445,7 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(Gemm
 constexpr int kGridCus = 256;
 
 #ifndef VSS_LT_CFG
-#define VSS_LT_CFG 256  // 256: 256 x 256 blocks where n % 256 == 0 (else 128 x 128); 128: always 128 x 128
+#define VSS_LT_CFG 256  // 256: 256 x 256 blocks for masked shapes with n % 256 == 0; 128: always 128 x 128
 #endif
 
 // the launch plan of one GEMM: kernel, output tiles, grid
@@ -428,9 +455,13 @@ struct Plan {
   int64_t tiles, grid;
 };
 
-static Plan plan(int64_t rows, int32_t n) {
+static Plan plan(int64_t rows, int32_t k, int32_t n) {
   Plan pl;
-  pl.kind = (VSS_LT_CFG == 256 && n % 256 == 0) ? 1 : 0;
+  // Exact shapes (rows % 128 == 0, K % 32 == 0: the update's layers but the first) run the
+  // 128 x 128 blocks with unmasked, pipelined loads (fastest there); the masked form is fastest on
+  // 256 x 256 blocks (profiles/r01_gemm_fused_bench.log).
+  const bool exact = VSS_LT_EXACT && rows % Cfg128::BM == 0 && k % kKS == 0;
+  pl.kind = (VSS_LT_CFG == 256 && !exact && n % 256 == 0) ? 1 : 0;
   static const int BMs[2] = {Cfg128::BM, Cfg256::BM};
   static const int BNs[2] = {Cfg128::BN, Cfg256::BN};
   static const int BPC[2] = {Cfg128::BLOCKS_PER_CU, Cfg256::BLOCKS_PER_CU};
@@ -454,16 +485,25 @@ static bool shape_ok(int64_t rows, int32_t k, int32_t n) {
          n <= 65536 && (rows + 127) / 128 * (n / 128) <= 0x7fff0000;  // tile + grid stays in int
 }
 
+template <int EPI, bool EXACT>
+static void launch_kind(const GemmArgs& a, const Plan& pl, hipStream_t s) {
+  const dim3 grid((unsigned)pl.grid);
+  if (pl.kind == 1)
+    hipLaunchKernelGGL((gemm_kernel<EPI, Cfg256, EXACT>), grid, dim3(Cfg256::THREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_kernel<EPI, Cfg128, EXACT>), grid, dim3(Cfg128::THREADS), 0, s, a);
+}
+
 template <int EPI>
 static int launch(void* stream, const GemmArgs& a0, const Plan& pl) {
   GemmArgs a = a0;
   a.tiles = pl.tiles;
-  const dim3 grid((unsigned)pl.grid);
-  hipStream_t s = (hipStream_t)stream;
-  switch (pl.kind) {
-    case 1: hipLaunchKernelGGL((gemm_kernel<EPI, Cfg256>), grid, dim3(Cfg256::THREADS), 0, s, a); break;
-    default: hipLaunchKernelGGL((gemm_kernel<EPI, Cfg128>), grid, dim3(Cfg128::THREADS), 0, s, a); break;
-  }
+  const int bm = pl.kind == 1 ? Cfg256::BM : Cfg128::BM;
+  const bool exact = VSS_LT_EXACT && a.rows % bm == 0 && a.k % kKS == 0;
+  if (exact)
+    launch_kind<EPI, true>(a, pl, (hipStream_t)stream);
+  else
+    launch_kind<EPI, false>(a, pl, (hipStream_t)stream);
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 
@@ -510,13 +550,13 @@ int vss_linear_tanh(void* stream, int64_t rows, int32_t k_in, int32_t n_out, con
     return VSS_E_ARG;
   if (rows == 0) return VSS_OK;
   const vgemm::GemmArgs a{rows, n_out, k_in, x, w, bias, nullptr, y, nullptr, 0};
-  return vgemm::launch<vgemm::EPI_TANH>(stream, a, vgemm::plan(rows, n_out));
+  return vgemm::launch<vgemm::EPI_TANH>(stream, a, vgemm::plan(rows, k_in, n_out));
 }
 
 int64_t vss_linear_tanh_backward_chunks(int64_t rows, int32_t k_next, int32_t n_out) {
   if (!vgemm::shape_ok(rows, k_next, n_out)) return -1;
   if (rows == 0) return 0;
-  const vgemm::Plan pl = vgemm::plan(rows, n_out);
+  const vgemm::Plan pl = vgemm::plan(rows, k_next, n_out);
   return pl.grid / (n_out / pl.bn);
 }
 
@@ -527,7 +567,7 @@ int vss_linear_tanh_backward(void* stream, int64_t rows, int32_t k_next, int32_t
     return VSS_E_ARG;
   if (rows == 0) return VSS_OK;
   const vgemm::GemmArgs a{rows, n_out, k_next, grad_next, w_next_t, nullptr, y, grad_in, bias_partial, 0};
-  return vgemm::launch<vgemm::EPI_DTANH>(stream, a, vgemm::plan(rows, n_out));
+  return vgemm::launch<vgemm::EPI_DTANH>(stream, a, vgemm::plan(rows, k_next, n_out));
 }
 
 }  // extern "C"

@@ -61,7 +61,9 @@ def parse():
     p.add_argument("--rollout-k", type=int, default=16,
                    help="also time vss_rollout with K steps per launch (0 = skip)")
     p.add_argument("--ppo-updates", type=int, default=None,
-                   help="PPO training updates timed after the env-step benchmark, on every rank (default 2)")
+                   help="PPO training updates run after the env-step benchmark, on every rank; the last one is "
+                        "timed (default 3: in this process the second update still carries warm-up, 4.2 s vs "
+                        "3.6 s steady state)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL) for real multi-GPU runs; gloo + --share-gpu to rehearse ranks on one GPU")
     p.add_argument("--share-gpu", action="store_true", help="map every rank to cuda:0 (rehearsal only)")
@@ -350,7 +352,7 @@ def main():
     # ---- the PPO train loop on every rank (its gradient all-reduce is the one real exchange
     # step of the path); after the env-step timing, before the rank-0-only legs ----
     ppo = None
-    ppo_updates = args.ppo_updates if args.ppo_updates is not None else 2
+    ppo_updates = args.ppo_updates if args.ppo_updates is not None else 3
     if ppo_updates > 0:
         if args.share_gpu:
             os.environ["VSS_LOCAL_DEVICE"] = "0"

@@ -91,7 +91,7 @@ def test_update_mlp_paths_cpu_match_autograd(mlp, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,n", [(52, 256), (256, 512), (512, 512), (512, 256), (8, 128)])
-@pytest.mark.parametrize("rows", [1, 127, 129, 4133, 70_000])
+@pytest.mark.parametrize("rows", [1, 127, 129, 4133, 70_000, 65_536])  # 65,536: exact shape, 4+ tiles per block
 def test_linear_tanh_gpu(rows, k, n):
     """vss_linear_tanh vs the fp32 torch op (addmm + tanh) and an fp64 reference: the fused GEMM
     sums in a different order and its tanh is within a few ulp, so within fp32 GEMM rounding."""
@@ -127,8 +127,8 @@ def test_linear_tanh_small_arguments_keep_relative_precision_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k_next,n", [(256, 512), (512, 512), (512, 256), (4, 128)])
-@pytest.mark.parametrize("rows", [1, 127, 129, 4133, 70_000])
+@pytest.mark.parametrize("k_next,n", [(256, 512), (512, 512), (512, 256), (4, 128), (64, 256)])
+@pytest.mark.parametrize("rows", [1, 127, 129, 4133, 70_000, 65_536])
 def test_linear_tanh_backward_gpu(rows, k_next, n):
     """vss_linear_tanh_backward vs fp64: gz = (gz_next @ w_next) * (1 - y^2) and db = gz.sum(0);
     deterministic (the same call twice gives the same bits)."""

@@ -191,11 +191,10 @@ class _LinearTanh(torch.autograd.Function):
 class _TanhMLP(torch.autograd.Function):
     """The Agent's MLP (ppo…:104-111: (Linear, Tanh) x L + Linear) as ONE autograd node for the
     update.  Forward: each hidden layer is vss_linear_tanh (GEMM + bias + tanh in one fp32 MFMA
-    launch); the output layer is addmm, as nn.Linear issues.  Backward: the output layer's input
-    gradient (a few columns) by torch's mm + the one-pass vss_tanh_grad_bias; every other hidden
-    tanh by vss_linear_tanh_backward (the input-gradient GEMM of the layer above with the tanh
-    derivative and the bias-gradient column sums in its epilogue); weight gradients split-K as
-    _LinearSplitK.  Inputs: x, W_0, b_0, ..., W_L, b_L."""
+    launch); the output layer is addmm, as nn.Linear issues.  Backward: every hidden tanh by
+    vss_linear_tanh_backward (the input-gradient GEMM of the layer above with the tanh derivative
+    and the bias-gradient column sums in its epilogue; the output layer's few columns zero-padded
+    to 4); weight gradients split-K as _LinearSplitK.  Inputs: x, W_0, b_0, ..., W_L, b_L."""
 
     @staticmethod
     def forward(ctx, x, *params):
@@ -218,10 +217,13 @@ class _TanhMLP(torch.autograd.Function):
             grads[2 * layer], grads[2 * layer + 1] = _split_k_wgrad(gz, hs[layer]), gb
             if layer == 0:
                 break
-            if layer == n - 1:
-                gz, gb = tanh_grad_bias(gz.mm(ws[layer]), hs[layer])
-            else:
-                gz, gb = linear_tanh_backward(gz, ws[layer], hs[layer])
+            w = ws[layer]
+            if layer == n - 1 and gz.shape[1] % 4:
+                # the output layer's few columns (1, 2 or 6): zero-padded to a multiple of 4, the
+                # GEMM's contraction granule, so this backward is one fused pass as well
+                pad = 4 - gz.shape[1] % 4
+                gz, w = nn.functional.pad(gz, (0, pad)), nn.functional.pad(w, (0, 0, 0, pad))
+            gz, gb = linear_tanh_backward(gz, w, hs[layer])
         gx = gz.mm(ws[0]) if ctx.needs_input_grad[0] else None
         return (gx, *grads)
 
@@ -242,8 +244,7 @@ def _fused_mlp_ok(seq: nn.Sequential) -> bool:
             not all(isinstance(a, nn.Tanh) for a in acts):
         return False
     return all(gemm_shape_ok(m.in_features, m.out_features) for m in lins[:-1]) and \
-        all(gemm_shape_ok(m.out_features, m.in_features) for m in lins[1:-1]) and \
-        lins[-1].in_features in TANH_GRAD_COLS
+        all(gemm_shape_ok((m.out_features + 3) // 4 * 4, m.in_features) for m in lins[1:])
 
 
 def _mlp_forward(seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define VSS_ABI_VERSION 1
+#define VSS_ABI_VERSION 2
 
 #define VSS_NUM_TEAMS 2          /* envs/vss.py:24 */
 #define VSS_NUM_ROBOTS 3         /* envs/vss.py:25 */
@@ -131,6 +131,29 @@ typedef struct vss_rollout_io {
   float* progress_f;
 } vss_rollout_io;
 
+/*
+ * Recorded random draws for the parity entries vss_step_replay / vss_reset_dones_replay: the
+ * reference's own torch draws, so the product kernels can be run against golden fixtures made by
+ * the reference (tests/golden/) instead of the Philox stream.  Per field f, row
+ * uniforms[f * uniform_stride ...] holds the draws the reference's reset_dones consumed for f in
+ * this call, in its order (envs/vss.py:267-333):
+ *   14 per rejection round r at [14 r, 14 r + 14): f's (7, 2) row of
+ *      torch.rand((len(close_ids), 7, 2)) (ball, then robots blue 0-2, yellow 0-2; x, y)
+ *      in the rounds where f was still too close (envs/vss.py:281-299);
+ *   then, after the R rounds f used, [14 R, 14 R + 6): f's row of torch_rand_float(-pi, pi,
+ *      (n, 6)) (robot yaws, envs/vss.py:307-312) and [14 R + 6, 14 R + 8): f's row of
+ *      torch.rand((n, 2)) (ball velocity, envs/vss.py:318-325).
+ * Rows of fields that do not reset are not read.  uniform_stride >= 22; a row holds
+ * (uniform_stride - 8) / 14 rounds (capped at 64, the product's bound).
+ * normals (SA/CMA/DMA; may be NULL in FULL): (n_fields, 12), the step's
+ * torch.normal(0, 0.15, (N, 2, 3, 2)) of random_ou (envs/wrappers.py:5-19), already scaled.
+ */
+typedef struct vss_replay_draws {
+  const float* uniforms;
+  int64_t uniform_stride;
+  const float* normals;
+} vss_replay_draws;
+
 /* ABI version (VSS_ABI_VERSION). */
 int vss_abi_version(void);
 
@@ -145,6 +168,14 @@ const char* vss_error_string(int code);
  */
 int vss_step(void* stream, int64_t n_fields, int32_t mode, const vss_params* params,
              const vss_state* st, const vss_step_io* io);
+
+/*
+ * Parity entry: vss_step with the reset and OU draws taken from `draws` (recorded reference
+ * draws, see vss_replay_draws) instead of the Philox stream.  The same kernel template as
+ * vss_step (REPLAY instantiation); everything but the draw source is shared.  Test use only.
+ */
+int vss_step_replay(void* stream, int64_t n_fields, int32_t mode, const vss_params* params,
+                    const vss_state* st, const vss_step_io* io, const vss_replay_draws* draws);
 
 /*
  * K consecutive FULL-mode steps in one launch for a pre-supplied action sequence (random-action
@@ -162,6 +193,11 @@ int vss_rollout(void* stream, int64_t n_fields, int32_t n_steps, const vss_param
  */
 int vss_reset_dones(void* stream, int64_t n_fields, const vss_params* params,
                     const vss_state* st);
+
+/* Parity entry: vss_reset_dones with recorded reference draws (e.g. the construction-time
+ * reset, envs/vss.py:72); normals unused.  Test use only. */
+int vss_reset_dones_replay(void* stream, int64_t n_fields, const vss_params* params,
+                           const vss_state* st, const vss_replay_draws* draws);
 
 /*
  * compute_obs (envs/vss.py:205-216, 530-575) for agents [0, n_agents): n_agents = 6 writes

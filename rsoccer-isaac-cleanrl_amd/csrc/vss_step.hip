@@ -624,20 +624,59 @@ __device__ __forceinline__ void coop_store_obs(float* __restrict__ out, int nv, 
   }
 }
 
-// ---- reset sampling (envs/vss.py:267-333), Philox counter (field, ctr, purpose<<24|round, blk) --
-__device__ __forceinline__ void reset_field(Bodies& b, uint32_t k0, uint32_t k1, uint32_t field, uint32_t ctr,
-                                            uint32_t ext) {
+// ---- reset sampling (envs/vss.py:267-333) --------------------------------------------------------------
+// Where the draws come from.  Product: Philox words, counter (field, ctr, purpose << 24 | round, block),
+// turned into U[0,1) by u01.  Replay (the parity entries vss_step_replay / vss_reset_dones_replay):
+// the field's row of recorded reference draws, `u[14 r + j]` = draw j of rejection round r (one
+// (7, 2) row of torch.rand((len(close_ids), 7, 2)), envs/vss.py:283-291), then at 14 R (R = rounds
+// used) the 6 yaw draws (torch_rand_float(-pi, pi, (n, 6)), envs/vss.py:307-312) and the 2 ball-
+// velocity draws (torch.rand((n, 2)), envs/vss.py:318-325).  A replayed word is the float's bit
+// pattern and its conversion the identity, so both sources run the same code below.
+struct ResetDraws {
+  uint32_t k0, k1, field, ctr, ext;
+  const float* u;  // replay: this field's row; product: unused
+  uint32_t rounds; // rejection rounds allowed (the replay row's capacity, else kMaxRejectRounds)
+};
+
+template <bool REPLAY>
+__device__ __forceinline__ float uval(uint32_t w) { return REPLAY ? __uint_as_float(w) : u01(w); }
+
+template <bool REPLAY>
+__device__ __forceinline__ void pos_block(const ResetDraws& d, uint32_t round, uint32_t blk, uint32_t o[4]) {
+  if constexpr (REPLAY) {
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint32_t j = 4u * blk + i;  // 14 draws per round: the 8th "entity" of block 3 is padding
+      o[i] = j < 14u ? __float_as_uint(d.u[14u * round + j]) : 0x3f000000u;
+    }
+  } else {
+    philox(d.k0, d.k1, d.field, d.ctr, ((kPurposePos | d.ext) << 24) | round, blk, o);
+  }
+}
+
+template <bool REPLAY>
+__device__ __forceinline__ void ang_block(const ResetDraws& d, uint32_t rounds_used, uint32_t blk, uint32_t o[4]) {
+  if constexpr (REPLAY) {
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) o[i] = __float_as_uint(d.u[14u * rounds_used + 4u * blk + i]);
+  } else {
+    philox(d.k0, d.k1, d.field, d.ctr, ((kPurposeAng | d.ext) << 24), blk, o);
+  }
+}
+
+template <bool REPLAY>
+__device__ __forceinline__ void reset_field(Bodies& b, const ResetDraws& d) {
   const float scale_x = 1.5f - 0.14f, scale_y = 1.3f - 0.14f;
   float px[7], py[7];
-  for (uint32_t round = 0;; ++round) {
+  uint32_t round = 0;
+  for (;; ++round) {
     uint32_t o[16];
 #pragma unroll
-    for (int blk = 0; blk < 4; ++blk)
-      philox(k0, k1, field, ctr, ((kPurposePos | ext) << 24) | round, (uint32_t)blk, o + 4 * blk);
+    for (int blk = 0; blk < 4; ++blk) pos_block<REPLAY>(d, round, (uint32_t)blk, o + 4 * blk);
 #pragma unroll
     for (int e = 0; e < 7; ++e) {
-      px[e] = (u01(o[2 * e]) - 0.5f) * scale_x;
-      py[e] = (u01(o[2 * e + 1]) - 0.5f) * scale_y;
+      px[e] = (uval<REPLAY>(o[2 * e]) - 0.5f) * scale_x;
+      py[e] = (uval<REPLAY>(o[2 * e + 1]) - 0.5f) * scale_y;
     }
     bool close = false;
 #pragma unroll
@@ -647,25 +686,25 @@ __device__ __forceinline__ void reset_field(Bodies& b, uint32_t k0, uint32_t k1,
         float dx = px[i] - px[j], dy = py[i] - py[j];
         close |= dx * dx + dy * dy < __uint_as_float(0x3ba0902du);  // == sqrtf(d2) < 0.07f (see below)
       }
-    if (!close || round + 1 >= (uint32_t)kMaxRejectRounds) break;
+    if (!close || round + 1 >= d.rounds) break;
   }
   b.bx = px[0]; b.by = py[0];
   uint32_t o[8];
-  philox(k0, k1, field, ctr, ((kPurposeAng | ext) << 24), 0u, o);
-  philox(k0, k1, field, ctr, ((kPurposeAng | ext) << 24), 1u, o + 4);
+  ang_block<REPLAY>(d, round + 1, 0u, o);
+  ang_block<REPLAY>(d, round + 1, 1u, o + 4);
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     b.x[r] = px[1 + r]; b.y[r] = py[1 + r];
     b.vx[r] = 0.0f; b.vy[r] = 0.0f; b.w[r] = 0.0f;
-    float ang = K_TWO_PI * u01(o[r]) + (-K_PI);
+    float ang = K_TWO_PI * uval<REPLAY>(o[r]) + (-K_PI);
     float sh, ch;
     sincos_small(ang * 0.5f, sh, ch);
     float nrm = sqrtf(sh * sh + ch * ch);
     b.qz[r] = sh / nrm;
     b.qw[r] = ch / nrm;
   }
-  b.bvx = u01(o[6]) - 0.5f;
-  b.bvy = u01(o[7]) - 0.5f;
+  b.bvx = uval<REPLAY>(o[6]) - 0.5f;
+  b.bvy = uval<REPLAY>(o[7]) - 0.5f;
 }
 
 // The same reset with the field's two lane halves (L, L + 32) sharing the work: each half draws
@@ -674,21 +713,22 @@ __device__ __forceinline__ void reset_field(Bodies& b, uint32_t k0, uint32_t k1,
 // compares squared distances with kMinDist2, the smallest float whose correctly rounded sqrtf is
 // >= 0.07f, so `d2 < kMinDist2` is exactly `sqrtf(d2) < 0.07f` (what reset_field and the oracle
 // evaluate) without the square roots.  Identical values in every lane to reset_field().
-__device__ __forceinline__ void reset_field_split(Bodies& b, uint32_t k0, uint32_t k1, uint32_t field, uint32_t ctr,
-                                                  uint32_t ext) {
+template <bool REPLAY>
+__device__ __forceinline__ void reset_field_split(Bodies& b, const ResetDraws& d) {
   const float kMinDist2 = __uint_as_float(0x3ba0902du);  // 0.0048999996f (tests/test_oracle_golden.py)
   const bool up = threadIdx.x >= 32;
   const uint32_t blk0 = up ? 2u : 0u;
   const float scale_x = 1.5f - 0.14f, scale_y = 1.3f - 0.14f;
   float px[8], py[8];
-  for (uint32_t round = 0;; ++round) {
+  uint32_t round = 0;
+  for (;; ++round) {
     uint32_t o[8];
-    philox(k0, k1, field, ctr, ((kPurposePos | ext) << 24) | round, blk0, o);
-    philox(k0, k1, field, ctr, ((kPurposePos | ext) << 24) | round, blk0 + 1u, o + 4);
+    pos_block<REPLAY>(d, round, blk0, o);
+    pos_block<REPLAY>(d, round, blk0 + 1u, o + 4);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {  // entities e (lower half) and 4 + e (upper half)
-      exch((u01(o[2 * e]) - 0.5f) * scale_x, px[e], px[4 + e]);
-      exch((u01(o[2 * e + 1]) - 0.5f) * scale_y, py[e], py[4 + e]);
+      exch((uval<REPLAY>(o[2 * e]) - 0.5f) * scale_x, px[e], px[4 + e]);
+      exch((uval<REPLAY>(o[2 * e + 1]) - 0.5f) * scale_y, py[e], py[4 + e]);
     }
     bool close = false;
 #pragma unroll
@@ -698,11 +738,11 @@ __device__ __forceinline__ void reset_field_split(Bodies& b, uint32_t k0, uint32
         float dx = px[i] - px[j], dy = py[i] - py[j];
         close |= dx * dx + dy * dy < kMinDist2;
       }
-    if (!close || round + 1 >= (uint32_t)kMaxRejectRounds) break;
+    if (!close || round + 1 >= d.rounds) break;
   }
   b.bx = px[0]; b.by = py[0];
   uint32_t oa[4], ang_u[8];
-  philox(k0, k1, field, ctr, ((kPurposeAng | ext) << 24), up ? 1u : 0u, oa);
+  ang_block<REPLAY>(d, round + 1, up ? 1u : 0u, oa);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float lo, hi;
@@ -712,7 +752,7 @@ __device__ __forceinline__ void reset_field_split(Bodies& b, uint32_t k0, uint32
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) {  // robots k (lower half) and k + 3 (upper half)
-    float ang = K_TWO_PI * u01(up ? ang_u[k + 3] : ang_u[k]) + (-K_PI);
+    float ang = K_TWO_PI * uval<REPLAY>(up ? ang_u[k + 3] : ang_u[k]) + (-K_PI);
     float sh, ch;
     sincos_small(ang * 0.5f, sh, ch);
     float nrm = sqrtf(sh * sh + ch * ch);
@@ -724,8 +764,8 @@ __device__ __forceinline__ void reset_field_split(Bodies& b, uint32_t k0, uint32
     b.x[r] = px[1 + r]; b.y[r] = py[1 + r];
     b.vx[r] = 0.0f; b.vy[r] = 0.0f; b.w[r] = 0.0f;
   }
-  b.bvx = u01(ang_u[6]) - 0.5f;
-  b.bvy = u01(ang_u[7]) - 0.5f;
+  b.bvx = uval<REPLAY>(ang_u[6]) - 0.5f;
+  b.bvy = uval<REPLAY>(ang_u[7]) - 0.5f;
 }
 
 // ---- rewards and dones (compute_rewards_and_dones, envs/vss.py:218-265, 578-655) --------------------
@@ -769,9 +809,14 @@ struct StepArgs {
   vss_params p;
   vss_state s;
   vss_step_io io;
+  vss_replay_draws rd;  // REPLAY instantiations only (vss_step_replay)
+  uint32_t rd_rounds;   // rejection rounds one replay row holds
 };
 
-template <int MODE>
+// REPLAY = false: the product kernel (Philox draws).  REPLAY = true: the parity entry
+// vss_step_replay, the same kernel consuming recorded reference draws (ResetDraws above; OU
+// normals from rd.normals) -- every other instruction is shared.
+template <int MODE, bool REPLAY = false>
 __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   constexpr int A = MODE == VSS_MODE_FULL ? 6 : (MODE == VSS_MODE_DMA ? 3 : 1);
   constexpr int R = MODE == VSS_MODE_DMA ? 3 : 1;
@@ -824,21 +869,30 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
     // random_ou (envs/wrappers.py:5-19): a <- clamp(a - 0.1 a + N(0, 0.15^2), -1, 1); the learner
     // slots (pairs 0 for SA, 0..2 for CMA/DMA) are overwritten, so their normals are not needed.
     constexpr int first_block = MODE == VSS_MODE_SA ? 0 : 1;
+    if constexpr (REPLAY) {
+      // torch.normal(0, 0.15, (N, 2, 3, 2)) of random_ou: the field's 12 recorded samples
+      if (valid) {
+        const float* z = args.rd.normals + f * 12;
 #pragma unroll
-    for (int blk = first_block; blk < 3; ++blk) {
-      uint32_t o[4];
-      philox(k0, k1, (uint32_t)f, ctr, kPurposeOU << 24, (uint32_t)blk, o);
+        for (int k = NL; k < 12; ++k) a[k] = clampf((a[k] - K_OU_THETA * a[k]) + z[k], -1.0f, 1.0f);
+      }
+    } else {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        int k = 4 * blk + 2 * h;
-        if (k < NL) continue;
-        float u1 = u01_open0(o[2 * h]);
-        float u2 = u01(o[2 * h + 1]);
-        float rad = sqrtf(-2.0f * logf_poly(u1));
-        float sz, cz;
-        sincos_turn(u2, sz, cz);
-        a[k] = clampf((a[k] - K_OU_THETA * a[k]) + K_OU_SIGMA * (rad * cz), -1.0f, 1.0f);
-        a[k + 1] = clampf((a[k + 1] - K_OU_THETA * a[k + 1]) + K_OU_SIGMA * (rad * sz), -1.0f, 1.0f);
+      for (int blk = first_block; blk < 3; ++blk) {
+        uint32_t o[4];
+        philox(k0, k1, (uint32_t)f, ctr, kPurposeOU << 24, (uint32_t)blk, o);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          int k = 4 * blk + 2 * h;
+          if (k < NL) continue;
+          float u1 = u01_open0(o[2 * h]);
+          float u2 = u01(o[2 * h + 1]);
+          float rad = sqrtf(-2.0f * logf_poly(u1));
+          float sz, cz;
+          sincos_turn(u2, sz, cz);
+          a[k] = clampf((a[k] - K_OU_THETA * a[k]) + K_OU_SIGMA * (rad * cz), -1.0f, 1.0f);
+          a[k + 1] = clampf((a[k + 1] - K_OU_THETA * a[k + 1]) + K_OU_SIGMA * (rad * sz), -1.0f, 1.0f);
+        }
       }
     }
     coop_load<NL>(args.io.actions + f0 * NL, nv, lds, lane);
@@ -890,8 +944,10 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   for (int k = 0; k < 12; ++k) dof[k] = a[k];
 #ifndef VSS_PROF_SKIP_RESET
   if (valid && done) {
-    if constexpr (kSplit) reset_field_split(b, k0, k1, (uint32_t)f, ctr, 0u);
-    else reset_field(b, k0, k1, (uint32_t)f, ctr, 0u);
+    const ResetDraws rd{k0, k1, (uint32_t)f, ctr, 0u, REPLAY ? args.rd.uniforms + f * args.rd.uniform_stride : nullptr,
+                        REPLAY ? args.rd_rounds : (uint32_t)kMaxRejectRounds};
+    if constexpr (kSplit) reset_field_split<REPLAY>(b, rd);
+    else reset_field<REPLAY>(b, rd);
 #pragma unroll
     for (int k = 0; k < 12; ++k) dof[k] = dof[k] * 0.0f;
   }
@@ -1073,8 +1129,9 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
 #pragma unroll
     for (int i = 0; i < 12; ++i) dof[i] = a[i];
     if (valid && done) {
-      if constexpr (kSplit) reset_field_split(b, k0, k1, (uint32_t)f, ctr + (uint32_t)k, 0u);
-      else reset_field(b, k0, k1, (uint32_t)f, ctr + (uint32_t)k, 0u);
+      const ResetDraws rd{k0, k1, (uint32_t)f, ctr + (uint32_t)k, 0u, nullptr, (uint32_t)kMaxRejectRounds};
+      if constexpr (kSplit) reset_field_split<false>(b, rd);
+      else reset_field<false>(b, rd);
 #pragma unroll
       for (int i = 0; i < 12; ++i) dof[i] = dof[i] * 0.0f;
     }
@@ -1113,13 +1170,18 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
 
 // External reset_dones: fields with reset_buf != 0 are re-sampled with the EXTERNAL purpose bit
 // and their rng counter advances (so repeated calls draw afresh).  dof_velocity_buf zeroed.
-__global__ __launch_bounds__(kWave) void reset_kernel(int64_t n, vss_params p, vss_state s) {
+// REPLAY: vss_reset_dones_replay, the recorded reference draws instead of Philox.
+template <bool REPLAY>
+__global__ __launch_bounds__(kWave) void reset_kernel(int64_t n, vss_params p, vss_state s, vss_replay_draws rdr,
+                                                     uint32_t rounds) {
   const int64_t f = (int64_t)blockIdx.x * kWave + threadIdx.x;
   if (f >= n || s.reset_buf[f] == 0) return;
   Bodies b;
   load_bodies(s.state, n, f, b);
   const uint32_t ctr = s.rng_counter[f];
-  reset_field(b, (uint32_t)p.seed, (uint32_t)(p.seed >> 32), (uint32_t)f, ctr, kExternal);
+  const ResetDraws rd{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), (uint32_t)f, ctr, kExternal,
+                      REPLAY ? rdr.uniforms + f * rdr.uniform_stride : nullptr, REPLAY ? rounds : (uint32_t)kMaxRejectRounds};
+  reset_field<REPLAY>(b, rd);
   store_bodies(s.state, n, f, b);
   s.rng_counter[f] = ctr + 1u;
 #pragma unroll
@@ -1176,6 +1238,58 @@ __global__ __launch_bounds__(256) void episode_stats_kernel(int64_t rows, const 
 // ================================================================================================
 // C ABI
 // ================================================================================================
+// Null or misaligned: the kernels move float4 / float2 vectors and int64 scalars.
+static bool bad(const void* ptr, uintptr_t align) { return !ptr || (reinterpret_cast<uintptr_t>(ptr) & (align - 1)); }
+static bool misaligned(const void* ptr, uintptr_t align) { return ptr && (reinterpret_cast<uintptr_t>(ptr) & (align - 1)); }
+
+static int check_state(int64_t n, const vss_state* st) {
+  if (n < 0 || n > (int64_t(1) << 26) || !st) return VSS_E_ARG;
+  if (bad(st->state, 4) || bad(st->progress_buf, 8) || bad(st->reset_buf, 8) || bad(st->dof_velocity_buf, 16) ||
+      bad(st->rng_counter, 4))
+    return VSS_E_ARG;
+  return VSS_OK;
+}
+
+static int launch_status() { return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH; }
+
+static int replay_rounds(const vss_replay_draws* d) {
+  if (!d || bad(d->uniforms, 4) || d->uniform_stride < 22 || d->uniform_stride > (int64_t(1) << 20)) return -1;
+  const int64_t r = (d->uniform_stride - 8) / 14;
+  return (int)(r < vss::kMaxRejectRounds ? r : vss::kMaxRejectRounds);
+}
+
+template <bool REPLAY>
+static int step_impl(void* stream, int64_t n, int32_t mode, const vss_params* p, const vss_state* st,
+                     const vss_step_io* io, const vss_replay_draws* rd) {
+  if (int rc = check_state(n, st)) return rc;
+  if (!p || !io || mode < VSS_MODE_FULL || mode > VSS_MODE_DMA) return VSS_E_ARG;
+  if (bad(io->actions, mode == VSS_MODE_FULL ? 16 : 8) || bad(io->obs, 16) || bad(io->terminal_obs, 16) ||
+      bad(io->rew, 16) || bad(io->time_outs, 1) || bad(io->progress_f, 4) || misaligned(io->reward_sum, 4) ||
+      misaligned(io->ou_buf, 16) || misaligned(io->dones_rep, 8))
+    return VSS_E_ARG;
+  if (mode != VSS_MODE_FULL && (!io->ou_buf || !io->reward_sum)) return VSS_E_ARG;
+  if (mode == VSS_MODE_DMA && !io->dones_rep) return VSS_E_ARG;
+  int rounds = 0;
+  if (REPLAY) {
+    rounds = replay_rounds(rd);
+    if (rounds < 1 || (mode != VSS_MODE_FULL && bad(rd->normals, 4))) return VSS_E_ARG;
+  }
+  if (n == 0) return VSS_OK;
+  vss::StepArgs args{n, *p, *st, *io, REPLAY ? *rd : vss_replay_draws{}, (uint32_t)rounds};
+  const int fpw = mode == VSS_MODE_FULL ? vss::fields_per_wave<VSS_MODE_FULL>()
+                  : mode == VSS_MODE_SA ? vss::fields_per_wave<VSS_MODE_SA>()
+                  : mode == VSS_MODE_CMA ? vss::fields_per_wave<VSS_MODE_CMA>() : vss::fields_per_wave<VSS_MODE_DMA>();
+  const dim3 grid((unsigned)((n + fpw - 1) / fpw)), block(vss::kWave);
+  hipStream_t s = (hipStream_t)stream;
+  switch (mode) {
+    case VSS_MODE_FULL: hipLaunchKernelGGL((vss::step_kernel<VSS_MODE_FULL, REPLAY>), grid, block, 0, s, args); break;
+    case VSS_MODE_SA: hipLaunchKernelGGL((vss::step_kernel<VSS_MODE_SA, REPLAY>), grid, block, 0, s, args); break;
+    case VSS_MODE_CMA: hipLaunchKernelGGL((vss::step_kernel<VSS_MODE_CMA, REPLAY>), grid, block, 0, s, args); break;
+    default: hipLaunchKernelGGL((vss::step_kernel<VSS_MODE_DMA, REPLAY>), grid, block, 0, s, args); break;
+  }
+  return launch_status();
+}
+
 extern "C" {
 
 int vss_abi_version(void) { return VSS_ABI_VERSION; }
@@ -1199,44 +1313,14 @@ const char* vss_error_string(int code) {
   }
 }
 
-// Null or misaligned: the kernels move float4 / float2 vectors and int64 scalars.
-static bool bad(const void* ptr, uintptr_t align) { return !ptr || (reinterpret_cast<uintptr_t>(ptr) & (align - 1)); }
-static bool misaligned(const void* ptr, uintptr_t align) { return ptr && (reinterpret_cast<uintptr_t>(ptr) & (align - 1)); }
-
-static int check_state(int64_t n, const vss_state* st) {
-  if (n < 0 || n > (int64_t(1) << 26) || !st) return VSS_E_ARG;
-  if (bad(st->state, 4) || bad(st->progress_buf, 8) || bad(st->reset_buf, 8) || bad(st->dof_velocity_buf, 16) ||
-      bad(st->rng_counter, 4))
-    return VSS_E_ARG;
-  return VSS_OK;
-}
-
-static int launch_status() { return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH; }
-
 int vss_step(void* stream, int64_t n, int32_t mode, const vss_params* p, const vss_state* st,
              const vss_step_io* io) {
-  if (int rc = check_state(n, st)) return rc;
-  if (!p || !io || mode < VSS_MODE_FULL || mode > VSS_MODE_DMA) return VSS_E_ARG;
-  if (bad(io->actions, mode == VSS_MODE_FULL ? 16 : 8) || bad(io->obs, 16) || bad(io->terminal_obs, 16) ||
-      bad(io->rew, 16) || bad(io->time_outs, 1) || bad(io->progress_f, 4) || misaligned(io->reward_sum, 4) ||
-      misaligned(io->ou_buf, 16) || misaligned(io->dones_rep, 8))
-    return VSS_E_ARG;
-  if (mode != VSS_MODE_FULL && (!io->ou_buf || !io->reward_sum)) return VSS_E_ARG;
-  if (mode == VSS_MODE_DMA && !io->dones_rep) return VSS_E_ARG;
-  if (n == 0) return VSS_OK;
-  vss::StepArgs args{n, *p, *st, *io};
-  const int fpw = mode == VSS_MODE_FULL ? vss::fields_per_wave<VSS_MODE_FULL>()
-                  : mode == VSS_MODE_SA ? vss::fields_per_wave<VSS_MODE_SA>()
-                  : mode == VSS_MODE_CMA ? vss::fields_per_wave<VSS_MODE_CMA>() : vss::fields_per_wave<VSS_MODE_DMA>();
-  const dim3 grid((unsigned)((n + fpw - 1) / fpw)), block(vss::kWave);
-  hipStream_t s = (hipStream_t)stream;
-  switch (mode) {
-    case VSS_MODE_FULL: hipLaunchKernelGGL(vss::step_kernel<VSS_MODE_FULL>, grid, block, 0, s, args); break;
-    case VSS_MODE_SA: hipLaunchKernelGGL(vss::step_kernel<VSS_MODE_SA>, grid, block, 0, s, args); break;
-    case VSS_MODE_CMA: hipLaunchKernelGGL(vss::step_kernel<VSS_MODE_CMA>, grid, block, 0, s, args); break;
-    default: hipLaunchKernelGGL(vss::step_kernel<VSS_MODE_DMA>, grid, block, 0, s, args); break;
-  }
-  return launch_status();
+  return step_impl<false>(stream, n, mode, p, st, io, nullptr);
+}
+
+int vss_step_replay(void* stream, int64_t n, int32_t mode, const vss_params* p, const vss_state* st,
+                    const vss_step_io* io, const vss_replay_draws* draws) {
+  return step_impl<true>(stream, n, mode, p, st, io, draws);
 }
 
 int vss_rollout(void* stream, int64_t n, int32_t k_steps, const vss_params* p, const vss_state* st,
@@ -1258,7 +1342,20 @@ int vss_reset_dones(void* stream, int64_t n, const vss_params* p, const vss_stat
   if (!p) return VSS_E_ARG;
   if (n == 0) return VSS_OK;
   const dim3 grid((unsigned)((n + vss::kWave - 1) / vss::kWave)), block(vss::kWave);
-  hipLaunchKernelGGL(vss::reset_kernel, grid, block, 0, (hipStream_t)stream, n, *p, *st);
+  hipLaunchKernelGGL(vss::reset_kernel<false>, grid, block, 0, (hipStream_t)stream, n, *p, *st, vss_replay_draws{},
+                     (uint32_t)vss::kMaxRejectRounds);
+  return launch_status();
+}
+
+int vss_reset_dones_replay(void* stream, int64_t n, const vss_params* p, const vss_state* st,
+                           const vss_replay_draws* draws) {
+  if (int rc = check_state(n, st)) return rc;
+  const int rounds = replay_rounds(draws);
+  if (!p || rounds < 1) return VSS_E_ARG;
+  if (n == 0) return VSS_OK;
+  const dim3 grid((unsigned)((n + vss::kWave - 1) / vss::kWave)), block(vss::kWave);
+  hipLaunchKernelGGL(vss::reset_kernel<true>, grid, block, 0, (hipStream_t)stream, n, *p, *st, *draws,
+                     (uint32_t)rounds);
   return launch_status();
 }
 

@@ -18,12 +18,13 @@ LIB_PATH = os.path.join(HERE, "libvss_amd.so")
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "vss.h")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MODE_FULL, MODE_SA, MODE_CMA, MODE_DMA = 0, 1, 2, 3
 STATE_CHANNELS = 58
 CH_BALL_X, CH_BALL_Y, CH_BALL_VX, CH_BALL_VY = 0, 1, 2, 3
 CH_RX, CH_RY, CH_RQX, CH_RQY, CH_RQZ, CH_RQW, CH_RVX, CH_RVY, CH_RW = 4, 10, 16, 22, 28, 34, 40, 46, 52
-EXPORTED = ("vss_abi_version", "vss_error_string", "vss_step", "vss_rollout", "vss_reset_dones",
+EXPORTED = ("vss_abi_version", "vss_error_string", "vss_step", "vss_step_replay", "vss_rollout", "vss_reset_dones",
+            "vss_reset_dones_replay",
             "vss_compute_observations", "vss_mlp_packed_size", "vss_mlp_pack", "vss_policy_forward",
             "vss_value_forward_masked", "vss_episode_stats", "vss_tanh_grad_chunks", "vss_tanh_grad_bias",
             "vss_linear_tanh", "vss_linear_tanh_backward_chunks", "vss_linear_tanh_backward")
@@ -57,6 +58,11 @@ class VssRolloutIO(ctypes.Structure):
                 ("actions", "obs", "terminal_obs", "rew", "dones", "time_outs", "progress_f")]
 
 
+class VssReplayDraws(ctypes.Structure):
+    """Recorded reference draws for the parity entries (include/vss.h vss_replay_draws)."""
+    _fields_ = [("uniforms", ctypes.c_void_p), ("uniform_stride", ctypes.c_int64), ("normals", ctypes.c_void_p)]
+
+
 class NativeError(RuntimeError):
     pass
 
@@ -80,6 +86,10 @@ def load() -> ctypes.CDLL:
     L.vss_error_string.restype = ctypes.c_char_p
     L.vss_step.argtypes = [P, i64, i32, P, P, P]
     L.vss_step.restype = ctypes.c_int
+    L.vss_step_replay.argtypes = [P, i64, i32, P, P, P, P]
+    L.vss_step_replay.restype = ctypes.c_int
+    L.vss_reset_dones_replay.argtypes = [P, i64, P, P, P]
+    L.vss_reset_dones_replay.restype = ctypes.c_int
     L.vss_rollout.argtypes = [P, i64, i32, P, P, P]
     L.vss_rollout.restype = ctypes.c_int
     L.vss_reset_dones.argtypes = [P, i64, P, P]

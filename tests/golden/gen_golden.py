@@ -288,6 +288,7 @@ class Recorder:
     def __init__(self):
         self.uniforms: list[np.ndarray] = []
         self.normals: list[np.ndarray] = []
+        self.u_sizes: list[int] = []  # size of every torch.rand call (the reference's batch shapes)
         self._rand, self._normal, self._tensor = torch.rand, torch.normal, torch.tensor
 
     def install(self):
@@ -297,6 +298,7 @@ class Recorder:
             k.pop("device", None)
             out = rec._rand(*a, **k)
             rec.uniforms.append(out.detach().reshape(-1).numpy().copy())
+            rec.u_sizes.append(out.numel())
             return out
 
         def normal(*a, **k):
@@ -317,6 +319,12 @@ class Recorder:
         z = np.concatenate(self.normals) if self.normals else np.zeros(0, np.float32)
         self.uniforms, self.normals = [], []
         return u.astype(np.float32), z.astype(np.float32)
+
+    def take_sizes(self) -> np.ndarray:
+        """Sizes of the torch.rand calls since the last call (rejection rounds, yaws, ball vel)."""
+        out = np.array(self.u_sizes, np.int64)
+        self.u_sizes = []
+        return out
 
 
 # ----------------------------------------------------------------------------------------------
@@ -453,12 +461,18 @@ def gen_obs_and_rewards(rec: Recorder):
     print("G1-G3: obs", tuple(obs.shape), "edge balls", m)
 
 
-def gen_full_rollout(rec: Recorder, n=8, steps=160, max_len=40):
-    """G4: the reference's VSS.step bookkeeping over `steps` steps, physics = oracle hook."""
+def gen_full_rollout(rec: Recorder, n=16, steps=1000, max_len=400):
+    """G4 (BASELINE config 1: 16 fields, random actions, 1,000 steps): the reference's VSS.step
+    bookkeeping, physics = oracle hook.  Goals are forced (play.py-style external writes through
+    the reference's views) into a field still in its first episode at steps max_len - 3 and
+    max_len - 2 -- the time-out edge (time_outs = progress >= max_len - 1 & reset) -- and into a
+    few more fields later on."""
     torch.manual_seed(1)
     rec.take()
+    rec.take_sizes()
     env = make_env(n, max_len)
     init_u, _ = rec.take()  # draws of the construction-time reset_dones (envs/vss.py:72)
+    init_sizes = rec.take_sizes()
     init_state = root_to_state(env.root_state.reshape(-1, 13), n)
     # external writes (play.py-style, through the reference's views) to force goals
     env.ball_pos[0] = torch.tensor([0.70, 0.05]); env.ball_vel[0] = torch.tensor([1.0, 0.0])
@@ -468,20 +482,31 @@ def gen_full_rollout(rec: Recorder, n=8, steps=160, max_len=40):
     gen = np.random.default_rng(7)
     keep = {k: [] for k in ("actions", "state", "rew", "reset", "progress", "time_outs", "progress_f",
                             "dof", "u_count")}
-    obs_steps, obs_keep, tobs_keep, uniforms = [], [], [], []
+    obs_steps, obs_keep, tobs_keep, uniforms, u_sizes, u_ncalls = [], [], [], [], [], []
+    forced_steps, forced_fields, forced_state = [], [], []
+    edge = {max_len - 3: None, max_len - 2: None}
     for t in range(steps):
         a = gen.uniform(-1.3, 1.3, (n, 2, 3, 2)).astype(np.float32)  # > clip to exercise clamp
-        if t in (max_len - 3, max_len - 2):
-            # goals at progress max_len-2 (field 3) and max_len-1 (field 2): the time-out edge
-            # (time_outs = progress >= max_len - 1 & reset), plus a third goal on the left
-            f = 3 if t == max_len - 3 else 2
-            env.ball_pos[f] = torch.tensor([0.74, 0.0]); env.ball_vel[f] = torch.tensor([1.0, 0.0])
-            env.ball_pos[4] = torch.tensor([-0.74, 0.1]); env.ball_vel[4] = torch.tensor([-1.0, 0.0])
+        push = []
+        if t in edge:  # a field still in its first episode (progress == t before this step)
+            cand = [f for f in range(n) if int(env.progress_buf[f]) == t and f not in edge.values()]
+            edge[t] = cand[0]
+            push = [(cand[0], 1.0), ((cand[0] + 5) % n, -1.0)]
+        elif t % 97 == 50:
+            push = [(t % n, 1.0 if t % 2 else -1.0)]
+        if push:
+            for f, side in push:
+                env.ball_pos[f] = torch.tensor([0.74 * side, 0.05]); env.ball_vel[f] = torch.tensor([1.0 * side, 0.0])
             env.gym.set_actor_root_state_tensor(env.sim, env.root_state)
-            keep.setdefault("forced", []).append(root_to_state(env.root_state.reshape(-1, 13), n)[LIVE])
+            forced_steps.append(t)
+            forced_fields.append(edge.get(t) if t in edge else -1)
+            forced_state.append(root_to_state(env.root_state.reshape(-1, 13), n)[LIVE])
         obs_dict, rew, reset, extras = env.step(torch.from_numpy(a))
         u, _ = rec.take()
+        sz = rec.take_sizes()
         uniforms.append(u)
+        u_sizes.append(sz)
+        u_ncalls.append(len(sz))
         keep["actions"].append(a.reshape(n, 12))
         keep["state"].append(root_to_state(env.root_state.reshape(-1, 13), n)[LIVE])
         keep["rew"].append(rew.numpy().reshape(n, 24).copy())
@@ -495,16 +520,19 @@ def gen_full_rollout(rec: Recorder, n=8, steps=160, max_len=40):
             obs_steps.append(t)
             obs_keep.append(obs_dict["obs"].numpy().reshape(n, 312).copy())
             tobs_keep.append(extras["terminal_observation"].numpy().reshape(n, 312).copy())
-    forced = np.stack(keep.pop("forced"))
     out = {k: np.stack(v) for k, v in keep.items()}
     np.savez_compressed(
-        os.path.join(HERE, "g4_full_rollout.npz"), forced_steps=np.array([max_len - 3, max_len - 2]),
-        forced_state=forced, init_uniforms=init_u, init_state=init_state,
+        os.path.join(HERE, "g4_full_rollout.npz"), forced_steps=np.array(forced_steps),
+        forced_fields=np.array(forced_fields), forced_state=np.stack(forced_state),
+        edge_steps=np.array(sorted(edge)), edge_fields=np.array([edge[k] for k in sorted(edge)]),
+        init_uniforms=init_u, init_u_sizes=init_sizes, init_state=init_state,
         start_state=start_state, live_channels=np.array(LIVE), uniforms=np.concatenate(uniforms),
+        u_sizes=np.concatenate(u_sizes), u_ncalls=np.array(u_ncalls),
         obs_steps=np.array(obs_steps), obs=np.stack(obs_keep), terminal_obs=np.stack(tobs_keep),
         max_len=np.array(max_len), **out)
-    print("G4: steps", steps, "resets", int(out["reset"].sum()), "goals",
-          int((np.abs(out["rew"][:, :, 0]) > 0).sum()), "obs steps", len(obs_steps))
+    print("G4: fields", n, "steps", steps, "resets", int(out["reset"].sum()), "goals",
+          int((np.abs(out["rew"][:, :, 0]) > 0).sum()), "time-outs", int(out["time_outs"].sum()),
+          "obs steps", len(obs_steps))
 
 
 def gen_wrapped(rec: Recorder, mode: str, n=6, steps=60, max_len=25):
@@ -512,8 +540,10 @@ def gen_wrapped(rec: Recorder, mode: str, n=6, steps=60, max_len=25):
     from envs.wrappers import SingleAgent, CMA, DMA
     torch.manual_seed(3)
     rec.take()
+    rec.take_sizes()
     env = make_env(n, max_len)
     init_u, _ = rec.take()
+    init_sizes = rec.take_sizes()
     init_state = root_to_state(env.root_state.reshape(-1, 13), n)
     W = {"sa": SingleAgent, "cma": CMA, "dma": DMA}[mode](env)
     rows = n * 3 if mode == "dma" else n
@@ -521,12 +551,13 @@ def gen_wrapped(rec: Recorder, mode: str, n=6, steps=60, max_len=25):
     gen = np.random.default_rng(11)
     keep = {k: [] for k in ("actions", "obs", "terminal_obs", "reward", "rews", "dones", "time_outs",
                             "progress_f", "state", "action_buf", "n_u", "n_z")}
-    U, Z = [], []
+    U, Z, S, NC = [], [], [], []
     for t in range(steps):
         a = gen.uniform(-1.2, 1.2, (rows, adim)).astype(np.float32)
         obs, reward, dones, info = W.step(torch.from_numpy(a))
         u, z = rec.take()
-        U.append(u); Z.append(z)
+        sz = rec.take_sizes()
+        U.append(u); Z.append(z); S.append(sz); NC.append(len(sz))
         keep["actions"].append(a)
         keep["obs"].append(obs["obs"].numpy().copy())
         keep["terminal_obs"].append(info["terminal_observation"].numpy().copy())
@@ -539,7 +570,8 @@ def gen_wrapped(rec: Recorder, mode: str, n=6, steps=60, max_len=25):
         keep["action_buf"].append(W.action_buf.numpy().reshape(n, 12).copy())
         keep["n_u"].append(len(u)); keep["n_z"].append(len(z))
     out = {k: np.stack(v) for k, v in keep.items()}
-    np.savez_compressed(os.path.join(HERE, f"g5_wrapped_{mode}.npz"), init_uniforms=init_u,
+    np.savez_compressed(os.path.join(HERE, f"g5_wrapped_{mode}.npz"), init_uniforms=init_u, init_u_sizes=init_sizes,
+                        u_sizes=np.concatenate(S), u_ncalls=np.array(NC),
                         init_state=init_state, uniforms=np.concatenate(U), normals=np.concatenate(Z),
                         live_channels=np.array(LIVE), max_len=np.array(max_len), num_envs=np.array(W.num_envs),
                         **out)

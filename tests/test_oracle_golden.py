@@ -18,7 +18,9 @@ TRIG_ATOL = 2e-6
 
 
 def load(golden_dir, name):
-    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+    """All arrays of a fixture, decompressed once (an NpzFile re-reads a key on every access)."""
+    with np.load(os.path.join(golden_dir, name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
 
 
 def obs_trig_mask():
@@ -110,8 +112,8 @@ def test_construction_reset_matches_reference(golden_dir):
 
 
 def test_full_step_bookkeeping_matches_reference(golden_dir):
-    """Teacher-forced replay of the reference's VSS.step (16 fields x 160 steps by default
-    config of the generator) -- progress / reset / time-out ordering, rewards, terminal obs,
+    """Teacher-forced replay of the reference's VSS.step over BASELINE config 1 (16 fields x
+    1,000 steps, random actions) -- progress / reset / time-out ordering, rewards, terminal obs,
     reset sampling order, dof zeroing (envs/vss.py:180-333, Ext VecTask.step)."""
     g = load(golden_dir, "g4_full_rollout.npz")
     live = g["live_channels"]
@@ -147,12 +149,14 @@ def test_full_step_bookkeeping_matches_reference(golden_dir):
         if t in obs_at:
             assert_obs_equal(io["obs"], g["obs"][obs_at[t]])
             assert_obs_equal(io["terminal_obs"], g["terminal_obs"][obs_at[t]])
+    assert (T, n) == (1000, 16), "G4 is BASELINE config 1: 16 fields x 1,000 steps"
     assert g["time_outs"].sum() > 0 and (np.abs(g["rew"][:, :, 0]) > 0).sum() > 0
     # the time-out edge: a goal at progress max_len-1 is a time-out, at max_len-2 it is not
     ml = int(g["max_len"])
-    t1, t2 = ml - 2, ml - 3
-    assert g["reset"][t1, 2] == 1 and g["time_outs"][t1, 2] == 1 and g["progress"][t1, 2] == ml - 1
-    assert g["reset"][t2, 3] == 1 and g["time_outs"][t2, 3] == 0 and g["progress"][t2, 3] == ml - 2
+    (t2, t1), (f2, f1) = g["edge_steps"], g["edge_fields"]
+    assert (t2, t1) == (ml - 3, ml - 2)
+    assert g["reset"][t1, f1] == 1 and g["time_outs"][t1, f1] == 1 and g["progress"][t1, f1] == ml - 1
+    assert g["reset"][t2, f2] == 1 and g["time_outs"][t2, f2] == 0 and g["progress"][t2, f2] == ml - 2
 
 
 # --------------------------------------------------------------------------------- G5
@@ -218,3 +222,35 @@ def test_reset_placement_threshold_is_exact():
     sweep = np.random.default_rng(0).uniform(0, 0.02, 200_000).astype(np.float32)
     for d2 in (around, sweep):
         assert np.array_equal(np.sqrt(d2) < c, d2 < t)
+
+
+# --------------------------------------------------------------------------------- replay rows
+def _reset_calls(g, steps_done):
+    """(flat draws, env_ids, call sizes) of every reset_dones call a fixture recorded."""
+    import replay_draws as RD
+    n = g["init_state"].shape[1]
+    sizes = RD.split_steps(g["u_sizes"], g["u_ncalls"])
+    counts = [int(s.sum()) for s in sizes]
+    yield g["init_uniforms"], np.arange(n), g["init_u_sizes"]
+    for t, flat in enumerate(RD.split_steps(g["uniforms"], counts)):
+        yield flat, np.nonzero(steps_done[t])[0], sizes[t]
+
+
+@pytest.mark.parametrize("name", ["g4_full_rollout.npz", "g5_wrapped_sa.npz", "g5_wrapped_cma.npz", "g5_wrapped_dma.npz"])
+def test_replay_rows_follow_reference_calls(golden_dir, name):
+    """tests/replay_draws.py regroups the reference's batch-ordered reset draws into the per-field
+    rows of vss_step_replay; the rejection rounds it derives must reproduce the sizes of every
+    torch.rand call the reference made (envs/vss.py:283-325) and consume every draw."""
+    import replay_draws as RD
+    g = load(golden_dir, name)
+    n = g["init_state"].shape[1]
+    done = g["reset"] if "reset" in g else g["dones"][:, ::3 if "dma" in name else 1]
+    calls = multi = 0
+    for flat, ids, sz in _reset_calls(g, done):
+        rows, rounds = RD.to_rows(flat, ids, n, call_sizes=sz)
+        calls += len(ids) > 0
+        multi += int((rounds > 1).sum())
+        assert (rounds[ids] >= 1).all() and (np.delete(rounds, ids) == 0).all()
+    assert calls >= 3, "fixture must exercise resets"
+    if name.startswith("g4"):
+        assert multi > 0, "G4 must exercise rejection re-draws (envs/vss.py:281-299)"

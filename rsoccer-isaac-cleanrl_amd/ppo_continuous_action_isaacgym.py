@@ -89,6 +89,10 @@ def parse_args(argv=None):
     p.add_argument("--evaluate", type=b, default=False, nargs="?", const=True,
                    help="after training, play matches vs the baseline teams (ppo…:380-461, no W&B)")
     p.add_argument("--eval-matches", type=int, default=10000, help="matches per baseline team")
+    p.add_argument("--global-adv-norm", type=b, default=True, nargs="?", const=True,
+                   help="with several ranks, normalise each minibatch's advantages with the mean / std "
+                        "of the GLOBAL minibatch (all ranks' rows, one small all-reduce), as the "
+                        "reference's single-process loop does (ppo…:324-326); off = per-rank statistics")
     p.add_argument("--amp", type=str, default="none", choices=["none", "bf16"],
                    help="bf16 autocast for the MLP GEMMs (off = the reference's fp32 numerics)")
     args = p.parse_args(argv)
@@ -377,6 +381,23 @@ def autocast(args, device):
     return torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=enabled)
 
 
+def normalize_advantages(mb_adv: torch.Tensor, world: int = 1, global_stats: bool = True) -> torch.Tensor:
+    """(a - mean) / (std + 1e-8) of ppo…:325-326.  One rank (or per-rank statistics): torch's own
+    mean / unbiased std, exactly the reference's expression.  Several ranks with global_stats:
+    the mean and unbiased std of the union of every rank's minibatch rows -- the minibatch the
+    reference would have drawn in one process -- from one all-reduce of (sum, sum of squares,
+    count) in float64."""
+    if world == 1 or not global_stats:
+        return (mb_adv - mb_adv.mean()) / (mb_adv.std() + 1e-8)
+    a = mb_adv.double()
+    s = torch.stack([a.sum(), (a * a).sum(), torch.tensor(float(a.numel()), dtype=torch.float64, device=a.device)])
+    dist.all_reduce(s)
+    n = s[2]
+    mean = s[0] / n
+    std = ((s[1] - n * mean * mean) / (n - 1)).clamp(min=0).sqrt()
+    return (mb_adv - mean.float()) / (std.float() + 1e-8)
+
+
 def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_advantages, b_returns,
                b_values, world=1, gen=None):
     """Clipped PPO over update_epochs x num_minibatches (ppo…:306-365).  Returns last-minibatch
@@ -404,7 +425,7 @@ def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_adv
                 clipfracs.append(((ratio - 1.0).abs() > args.clip_coef).float().mean())
             mb_adv = b_advantages[mb_inds]
             if args.norm_adv:
-                mb_adv = (mb_adv - mb_adv.mean()) / (mb_adv.std() + 1e-8)
+                mb_adv = normalize_advantages(mb_adv, world, getattr(args, "global_adv_norm", True))
             pg_loss = torch.max(-mb_adv * ratio, -mb_adv * torch.clamp(ratio, 1 - args.clip_coef, 1 + args.clip_coef)).mean()
             newvalue = newvalue.view(-1)
             if args.clip_vloss:

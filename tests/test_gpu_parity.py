@@ -165,6 +165,40 @@ def test_wrapped_step_free_running_bit_exact(mode, n):
     assert h.reset.sum() >= 0
 
 
+def test_dma_65536_fields_config4_bit_exact():
+    """BASELINE config 4: DMA at 65,536 fields = 196,608 agent rows (the reference needs
+    num_envs % 3 == 0, envs/wrappers.py:30), free-running with episodes short enough to reset,
+    every output bit-exact vs the oracle at full size, plus the DMA packing's shape contract."""
+    from envs.wrappers import DMA
+    n = 65536
+    env = make_vss(n, max_len=12, seed=31)
+    W = DMA(env)
+    assert W.num_envs == 3 * n and env.num_envs == 3 * n  # DMA re-assigns num_environments (wrappers.py:154)
+    h = host_from(env)
+    prm = oracle_params(env)
+    io = O.make_io(n, O.MODE_DMA)
+    gen = torch.Generator(device=DEV).manual_seed(8)
+    resets = 0
+    for t in range(26):
+        a = torch.rand((3 * n, 2), device=DEV, generator=gen) * 2.4 - 1.2
+        obs, reward, dones, info = W.step(a)
+        O.step(h, O.MODE_DMA, a.cpu().numpy(), io, prm)
+        msg = f"step {t}"
+        assert_env_equal(env, h, msg)
+        np.testing.assert_array_equal(bits(W.action_buf).reshape(n, 12), io["ou_buf"].view(np.uint32), err_msg=msg)
+        np.testing.assert_array_equal(bits(obs["obs"]), io["obs"].view(np.uint32), err_msg=msg)
+        np.testing.assert_array_equal(bits(info["terminal_observation"]), io["terminal_obs"].view(np.uint32), err_msg=msg)
+        np.testing.assert_array_equal(bits(info["rews"]), io["rew"].view(np.uint32), err_msg=msg)
+        np.testing.assert_array_equal(bits(reward), io["reward_sum"].view(np.uint32), err_msg=msg)
+        np.testing.assert_array_equal(dones.cpu().numpy(), io["dones_rep"], err_msg=msg)
+        np.testing.assert_array_equal(info["time_outs"].cpu().numpy().astype(np.uint8), io["time_outs"], err_msg=msg)
+        assert tuple(obs["obs"].shape) == (3 * n, 52) and tuple(reward.shape) == (3 * n,)
+        d = dones.view(n, 3)
+        assert torch.equal(d[:, 0], d[:, 1]) and torch.equal(d[:, 0], d[:, 2])  # repeat_interleave(3)
+        resets += int(h.reset.sum())
+    assert resets >= n  # every field has ended an episode at least once (max_len 12)
+
+
 def test_external_reset_play_style():
     """play.py:132-133: envs.reset_buf[:] = 1; envs.reset_dones() re-samples every field."""
     n = 512
@@ -375,3 +409,45 @@ def test_rollout_equals_sequential_steps_and_oracle(n, K):
         assert torch.equal(getattr(e1, name), getattr(e2, name)), name
     assert_env_equal(e2, h, "after rollout")
     assert int(out["dones"].sum()) > 0
+
+
+def test_returned_buffers_are_persistent_documented_semantics():
+    """obs_dict['obs'], rew_buf, reset_buf and extras[...] are persistent buffers
+    that the next step overwrites in place (the reference rebinds reset_buf and clones obs /
+    terminal obs, envs/vss.py:196,198,258-265); callers that keep a step's outputs must clone."""
+    n = 64
+    env = make_vss(n, max_len=5)
+    a = torch.zeros((n, 2, 3, 2), device=DEV)
+    o1, r1, d1, x1 = env.step(a)
+    kept = {k: t.clone() for k, t in (("obs", o1["obs"]), ("rew", r1), ("reset", d1),
+                                      ("term", x1["terminal_observation"]), ("prog", x1["progress_buffer"]))}
+    ptrs = (o1["obs"].data_ptr(), r1.data_ptr(), d1.data_ptr(), x1["terminal_observation"].data_ptr(),
+            x1["progress_buffer"].data_ptr(), x1["time_outs"].data_ptr())
+    for _ in range(4):  # progress reaches max_len: every field resets
+        o2, r2, d2, x2 = env.step(a)
+    assert ptrs == (o2["obs"].data_ptr(), r2.data_ptr(), d2.data_ptr(), x2["terminal_observation"].data_ptr(),
+                    x2["progress_buffer"].data_ptr(), x2["time_outs"].data_ptr())
+    assert o1["obs"] is o2["obs"] and d1 is env.reset_buf
+    assert not torch.equal(kept["reset"], d1) and not torch.equal(kept["prog"], x1["progress_buffer"])
+    assert not torch.equal(kept["obs"], o1["obs"])  # overwritten in place by the later steps
+
+
+@pytest.mark.parametrize("mode", [O.MODE_SA, O.MODE_DMA])
+def test_wrapped_modes_leave_vss_obs_and_rew_bufs_stale(mode):
+    """the fused SA/CMA/DMA kernels write only the learner rows into the wrapper's
+    own buffers; VSS.obs_buf / rew_buf keep their last FULL-mode contents (the reference's
+    wrappers never read them after slicing, envs/wrappers.py:101-180)."""
+    from envs.wrappers import DMA, SingleAgent
+    n = 64
+    env = make_vss(n)
+    W = (SingleAgent if mode == O.MODE_SA else DMA)(env)
+    before_obs, before_rew = env.obs_buf.clone(), env.rew_buf.clone()
+    rows = n * (3 if mode == O.MODE_DMA else 1)
+    for _ in range(3):
+        obs, reward, dones, info = W.step(torch.rand((rows, 2), device=DEV) * 2 - 1)
+    torch.cuda.synchronize()
+    assert torch.equal(env.obs_buf, before_obs) and torch.equal(env.rew_buf, before_rew)
+    # while the wrapper's outputs are current: they equal a fresh compute_obs of the blue rows
+    agents = 3 if mode == O.MODE_DMA else 1
+    fresh = env.compute_observations(torch.empty((n, agents, 52), device=DEV), agents)
+    assert torch.equal(obs["obs"].view(n, agents, 52), fresh)

@@ -92,14 +92,14 @@ def _synthetic_batch(seed, n=256):
         torch.randn(n, generator=g), torch.randn(n, generator=g)
 
 
-def _dp_worker(rank, world, port, q):
+def _dp_worker(rank, world, port, q, adv_norm="off"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
     agent = make_agent(2)
     flat = P.FlatGrads(agent)
     opt = torch.optim.Adam(agent.parameters(), lr=1e-3, eps=1e-5)
-    args = _args(norm_adv=False)
+    args = _args(norm_adv=adv_norm != "off", global_adv_norm=adv_norm == "global")
     obs, act, logp, adv, ret, val = _synthetic_batch(100 + rank)
     P.ppo_update(agent, opt, flat, args, obs, logp, act, adv, ret, val, world=world,
                  gen=torch.Generator().manual_seed(7))
@@ -115,14 +115,17 @@ def _free_port():
     return p
 
 
-def test_data_parallel_update_gloo_world2():
+@pytest.mark.parametrize("adv_norm", ["off", "local", "global"])
+def test_data_parallel_update_gloo_world2(adv_norm):
     """Two ranks with different local batches end with identical weights (one all-reduce per
     minibatch keeps replicas in sync), and those weights equal a single process that averages
-    the two ranks' gradients by hand."""
+    the two ranks' gradients by hand.  Advantage normalisation (ppo…:325-326): 'global' (the
+    default) normalises with the statistics of both ranks' minibatch rows together -- the
+    reference's one-process minibatch -- and 'local' with each rank's own."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q, adv_norm)) for r in range(2)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=240) for _ in procs)
@@ -142,12 +145,19 @@ def test_data_parallel_update_gloo_world2():
     for epoch in range(args.update_epochs):
         perms = [torch.randperm(256, generator=gg) for gg in gens]
         for start in range(0, 256, 128):
+            mbs = [perms[r][start:start + 128] for r in range(2)]
+            both = torch.cat([data[r][3][mbs[r]] for r in range(2)])  # the global minibatch's advantages
             for r in range(2):
                 obs, act, logp, adv, ret, val = data[r]
-                mb = perms[r][start:start + 128]
+                mb = mbs[r]
+                a = adv[mb]
+                if adv_norm == "local":
+                    a = (a - a.mean()) / (a.std() + 1e-8)
+                elif adv_norm == "global":
+                    a = (a - both.mean()) / (both.std() + 1e-8)
                 _, nl, ent, nv = agents[r].get_action_and_value(obs[mb], act[mb])
                 ratio = (nl - logp[mb]).exp()
-                pg = torch.max(-adv[mb] * ratio, -adv[mb] * torch.clamp(ratio, 0.8, 1.2)).mean()
+                pg = torch.max(-a * ratio, -a * torch.clamp(ratio, 0.8, 1.2)).mean()
                 vl = 0.5 * ((nv.view(-1) - ret[mb]) ** 2).mean()
                 loss = pg - args.ent_coef * ent.mean() + vl * args.vf_coef
                 flats[r].zero()
@@ -179,6 +189,24 @@ def test_train_end_to_end_gpu(env_id, tmp_path):
         tags = {line.split(",")[0] for line in open(os.path.join(run, "scalars.csv")).read().splitlines()[1:]}
         assert {"losses/value_loss", "losses/policy_loss", "losses/entropy", "losses/approx_kl",
                 "losses/clipfrac", "losses/learning_rate", "Charts/SPS"} <= tags
+
+
+@pytest.mark.gpu
+def test_train_sa_65536_envs_config3(tmp_path):
+    """BASELINE config 3: the full SA train loop at 65,536 envs with the reference's update
+    defaults (T = 128, 8 epochs x 4 minibatches, fp32), one update: finite losses, the timing
+    fields bench.py and the history report, every env-step counted, the entropy still near its
+    initial value (a sane first update)."""
+    args = P.parse_args(["--env-id", "sa", "--num-envs", "65536", "--num-updates", "1", "--save-path", str(tmp_path)])
+    assert (args.num_steps, args.update_epochs, args.num_minibatches) == (128, 8, 4)
+    agent, hist = P.train(args)
+    (h,) = hist
+    assert h["global_step"] == 65536 * 128
+    for k in ("v_loss", "pg_loss", "entropy", "approx_kl", "old_approx_kl", "clipfrac", "mean_return"):
+        assert np.isfinite(h[k]), (k, h)
+    assert h["rollout_s"] > 0 and h["update_s"] > 0 and h["sps"] > 0 and h["episodes"] > 0
+    assert abs(h["entropy"] - 2 * (0.5 + 0.5 * np.log(2 * np.pi))) < 0.1  # logstd starts at 0
+    assert 0 <= h["clipfrac"] <= 1 and h["approx_kl"] < 0.1
 
 
 @pytest.mark.gpu

@@ -13,12 +13,18 @@ and the max-over-ranks of the elapsed time.
 Rank 0 prints ONE JSON line (value = env-steps/s summed over all ranks = fields x ranks x K /
 max-over-ranks time).  `roofline.achieved` = algorithmic bytes per launch / mean launch time
 measured with HIP events on the launch stream; `cpu_baseline` = the C oracle (oracle/, the only
-use of it here) on the host's cores (one 4,096-field shard per thread, up to 16) over a bounded
-sample, with its one-thread rate beside it.
+use of it here) on the host's cores (one 4,096-field shard per thread, up to 16: 65,536 fields on a 16-core share) over a bounded
+sample, with one-thread rates at the SURVEY §8(d) shapes (16 fields x 1,000 steps = config 1,
+4,096 and 65,536 fields) beside it.  `past_l3` repeats the FULL timing at 131,072 fields, whose
+406 MB per launch cannot sit in the 256 MiB Infinity Cache, so its fraction is HBM-backed.
+`roofline.traffic` comes from the committed rocprofv3 PMC passes (profiles/pmc_traffic*.json,
+tools/pmc_summary.py) and is reported only if that profile was taken of the current
+csrc/vss_step.hip (source hash), else null.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -68,6 +74,8 @@ def parse():
                    help="nccl (= RCCL) for real multi-GPU runs; gloo + --share-gpu to rehearse ranks on one GPU")
     p.add_argument("--share-gpu", action="store_true", help="map every rank to cuda:0 (rehearsal only)")
     p.add_argument("--graph", type=int, default=0, help="replay the launches from a HIP graph (1) or launch eagerly (0)")
+    p.add_argument("--l3-check-fields", type=int, default=131072,
+                   help="FULL launches timed again at this many fields (past the 256 MiB Infinity Cache; 0 = skip)")
     return p.parse_args()
 
 
@@ -96,16 +104,43 @@ def host_threads() -> int:
     return max(1, min(16, avail))
 
 
+def _oracle_fixed(O, n: int, steps: int, seed: int = 1) -> float:
+    """One thread, n fields, exactly `steps` steps: env-steps/s."""
+    h = O.HostEnv(n)
+    prm = O.params(seed=seed)
+    O.reset_dones(h, prm)
+    io = O.make_io(n, O.MODE_FULL)
+    gen = np.random.default_rng(seed)
+    acts = [gen.uniform(-1, 1, (n, 12)).astype(np.float32) for _ in range(8)]
+    t0 = time.perf_counter()
+    for k in range(steps):
+        O.step(h, O.MODE_FULL, acts[k % 8], io, prm)
+    return n * steps / (time.perf_counter() - t0)
+
+
 def cpu_baseline(seconds: float):
-    """The C oracle on the same workload shape (FULL contract, random actions), 4,096 fields per
-    host thread: first one thread (≈1/3 of the budget), then one shard per available core
-    (≈2/3), which is the reported value."""
+    """The C oracle on the same workload shape (FULL contract, random actions).  Reported value:
+    one 4,096-field shard per available core (up to 16 = 65,536 fields), ≈1/2 of the budget.
+    Beside it, one thread at the SURVEY §8(d) shapes: 16 fields x 1,000 steps (config 1),
+    4,096 fields (≈1/4 of the budget) and 65,536 fields (≈1/4)."""
     import threading
 
     import oracle as O
     n = 4096
     res = {}
-    for threads, share in ((1, 1 / 3), (host_threads(), 2 / 3)):
+    shapes = {"16_fields_x_1000_steps_1_thread": _oracle_fixed(O, 16, 1000)}
+    t0 = time.perf_counter()
+    big_steps = 0
+    h = O.HostEnv(65536)
+    prm = O.params(seed=3)
+    O.reset_dones(h, prm)
+    io = O.make_io(65536, O.MODE_FULL)
+    a = np.random.default_rng(3).uniform(-1, 1, (65536, 12)).astype(np.float32)
+    while time.perf_counter() - t0 < seconds / 4 or big_steps < 2:
+        O.step(h, O.MODE_FULL, a, io, prm)
+        big_steps += 1
+    shapes["65536_fields_1_thread"] = 65536 * big_steps / (time.perf_counter() - t0)
+    for threads, share in ((1, 1 / 4), (host_threads(), 1 / 2)):
         counts = [0] * threads
         t0 = time.perf_counter()
         deadline = t0 + seconds * share
@@ -118,11 +153,52 @@ def cpu_baseline(seconds: float):
         res[threads if threads == 1 else "all"] = (n * sum(counts) / el, counts, el, threads)
     v1, c1, e1, _ = res[1]
     vn, cn, en, tn = res["all"]
+    shapes["4096_fields_1_thread"] = v1
+    shapes[f"{tn * n}_fields_{tn}_threads"] = vn
     return {"value": vn, "unit": "env-steps/s", "cores": tn, "kind": "port",
-            "single_thread_value": v1,
+            "single_thread_value": v1, "shapes": shapes,
             "sample": f"oracle/vss_oracle.c FULL contract, random actions, {tn} host threads x {n} fields "
                       f"({sum(cn)} shard-steps in {en:.1f} s; 1 thread: {n} fields x {c1[0]} steps in "
-                      f"{e1:.1f} s = {v1:.3g} env-steps/s), host CPU: {cpu_model()}"}
+                      f"{e1:.1f} s = {v1:.3g} env-steps/s; 65,536 fields x {big_steps} steps on 1 thread; "
+                      f"16 fields x 1,000 steps on 1 thread), host CPU: {cpu_model()}"}
+
+
+def step_source_sha() -> str:
+    with open(os.path.join(REPO, "rsoccer-isaac-cleanrl_amd", "csrc", "vss_step.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def past_l3_leg(n: int, steps: int, dev) -> dict:
+    """FULL launches at `n` fields (131,072 by default: 406 MB per launch, past the 256 MiB
+    Infinity Cache) timed with HIP events on the launch stream: the HBM-backed fraction."""
+    from envs.vss import VSS, default_cfg
+    from vss_amd import _native as N
+    cfg = default_cfg(n)
+    cfg["env"]["seed"] = 11
+    env = VSS(cfg, str(dev), str(dev), 0, True, False, False)
+    gen = torch.Generator(device=dev).manual_seed(77)
+    pool = [torch.rand((n, 12), device=dev, generator=gen) * 2 - 1 for _ in range(4)]
+    lib, stream = N.load(), N.stream_of(dev)
+    prm, st = env._c_params(), env._c_state()
+    cios = [N.VssStepIO(a.data_ptr(), None, N.ptr(env.obs_buf), N.ptr(env.terminal_obs_buf), N.ptr(env.rew_buf),
+                        None, None, N.ptr(env.timeout_buf), N.ptr(env.progress_f_buf)) for a in pool]
+    byref = N.ctypes.byref
+    for k in range(10):
+        N.check(lib.vss_step(stream, n, N.MODE_FULL, byref(prm), byref(st), byref(cios[k % 4])), "vss_step")
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for k in range(steps):
+        lib.vss_step(stream, n, N.MODE_FULL, byref(prm), byref(st), byref(cios[k % 4]))
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    algo = BYTES["full"] * n
+    del env
+    torch.cuda.empty_cache()
+    return {"fields": n, "launches": steps, "kernel_ms": ms, "algorithmic_bytes_per_launch": algo,
+            "achieved": algo / (ms * 1e-3) / 1e9, "unit": "GB/s", "frac": algo / (ms * 1e-3) / HBM_PEAK,
+            "env_steps_per_s": n / (ms * 1e-3)}
 
 
 def rollout_leg(env, K: int, steps: int, gen, dev) -> dict:
@@ -365,15 +441,20 @@ def main():
         value = n * world * args.steps / elapsed
         algo = BYTES[args.mode] * n
         achieved = algo / (kern_ms * 1e-3)
-        traffic = None
+        traffic, traffic_source = None, None
         # HBM bytes per launch from the committed rocprofv3 PMC passes of the same command
-        # (tools/pmc_summary.py; null when no profile matches this mode and size)
+        # (tools/pmc_summary.py); null unless that profile matches this mode and size AND was
+        # taken of the current kernel source (so a changed kernel cannot report stale traffic)
         tfile = os.path.join(REPO, "profiles", "pmc_traffic.json" if args.mode == "full" else f"pmc_traffic_{args.mode}.json")
         if os.path.exists(tfile):
             try:
                 tj = json.load(open(tfile))
-                if tj.get("fields") == n and tj.get("mode") == args.mode:
+                if tj.get("fields") == n and tj.get("mode") == args.mode and tj.get("source_sha") == step_source_sha():
                     traffic = tj.get("hbm_bytes_per_launch")
+                    traffic_source = (f"{os.path.relpath(tfile, REPO)} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes, "
+                                      f"tag {tj.get('tag')}, vss_step.hip sha {tj.get('source_sha')})")
+                else:
+                    traffic_source = f"{os.path.relpath(tfile, REPO)} does not match this kernel source / config: not used"
             except (OSError, ValueError):
                 traffic = None
         out = {
@@ -395,10 +476,12 @@ def main():
                        "launch": "hipGraph replay (16 captured steps)" if args.graph else "eager ctypes launches",
                        "parallelism": f"fields sharded over {world} GPU(s), no data-path collective"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_source": traffic_source,
                          "algorithmic_bytes_per_launch": algo, "kernel_ms": kern_ms,
                          "kernel_ms_per_launch_events": per_launch_ms},
         }
+        if args.l3_check_fields > 0 and mode == N.MODE_FULL:
+            out["past_l3"] = past_l3_leg(args.l3_check_fields, args.steps, dev)
         if args.rollout_k > 0 and mode == N.MODE_FULL:
             out["rollout"] = rollout_leg(env, args.rollout_k, args.steps, gen, dev)
         if mode == N.MODE_FULL:

@@ -31,13 +31,20 @@ case ",$STEPS," in *,bench,*) run bench 400 python bench.py; run bench_eager 300
 case ",$STEPS," in *,benchsa,*) run bench_sa 300 python bench.py --mode sa --no-cpu-baseline ;; esac
 case ",$STEPS," in *,prof,*)
   run rocprof_stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \
-      python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline ;;
+      python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline --l3-check-fields 0 ;;
 esac
 case ",$STEPS," in *,pmc,*)
   run rocprof_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$TAG" -o run -- \
-      python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline
+      python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --ppo-updates 0 --l3-check-fields 0 --rollout-k 0
   run rocprof_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$TAG" -o run -- \
-      python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+      python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --ppo-updates 0 --l3-check-fields 0 --rollout-k 0 ;;
+esac
+# the same two passes at 131,072 fields (406 MB per launch, past the 256 MiB Infinity Cache)
+case ",$STEPS," in *,pmcl3,*)
+  run rocprof_fetch_l3 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_l3_$TAG" -o run -- \
+      python3 bench.py --fields 131072 --steps 20 --warmup 5 --no-cpu-baseline --ppo-updates 0 --l3-check-fields 0 --rollout-k 0
+  run rocprof_write_l3 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_l3_$TAG" -o run -- \
+      python3 bench.py --fields 131072 --steps 20 --warmup 5 --no-cpu-baseline --ppo-updates 0 --l3-check-fields 0 --rollout-k 0 ;;
 esac
  case ",$STEPS," in *,ablate,*) run ablate 300 python tools/ablate.py ;; esac
 case ",$STEPS," in *,ablsa,*)

@@ -33,7 +33,7 @@ def counters(path, kernel_substr):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", default="r01")
-    ap.add_argument("--kernel", default="step_kernel<0>")
+    ap.add_argument("--kernel", default="step_kernel<0, false>")
     ap.add_argument("--fields", type=int, default=65536)
     ap.add_argument("--mode", default="full")
     ap.add_argument("--algo-bytes", type=int, default=3101)
@@ -44,16 +44,27 @@ def main():
     out_dir = os.path.join(REPO, "profiles")
     os.makedirs(out_dir, exist_ok=True)
     g = os.path.join(REPO, "gpurun_out")
-    res = {"tag": args.tag, "kernel": args.kernel, "fields": args.fields, "mode": args.mode}
+    import hashlib
+    with open(os.path.join(REPO, "rsoccer-isaac-cleanrl_amd", "csrc", "vss_step.hip"), "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    res = {"tag": args.tag, "kernel": args.kernel, "fields": args.fields, "mode": args.mode, "source_sha": sha}
 
     sdir = args.stats_dir or f"prof_{args.tag}"
     stats = os.path.join(g, sdir, "run_kernel_stats.csv")
+    trace = os.path.join(g, sdir, "run_kernel_trace.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(out_dir, f"{args.tag}_{sdir.replace('_' + args.tag, '')}_kernel_stats.csv"))
         for r in csv.DictReader(open(stats)):
             if args.kernel in r["Name"]:
                 res["avg_ns"] = float(r["AverageNs"])
                 res["calls"] = int(r["Calls"])
+    if os.path.exists(trace):
+        # the launches of this field count only (one 64-lane wave per 32 fields: grid = 2 x fields)
+        d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(trace))
+             if args.kernel in r["Kernel_Name"] and int(r["Grid_Size_X"]) == 2 * args.fields]
+        if d:
+            res["avg_ns"], res["calls"] = statistics.mean(d), len(d)
+            res["avg_ns_source"] = f"{sdir}/run_kernel_trace.csv, grid {2 * args.fields}"
     fpath = os.path.join(g, f"pmc_fetch{args.suffix}_{args.tag}", "run_counter_collection.csv")
     wpath = os.path.join(g, f"pmc_write{args.suffix}_{args.tag}", "run_counter_collection.csv")
     if os.path.exists(fpath) and os.path.exists(wpath):
@@ -68,7 +79,7 @@ def main():
         res["traffic_over_algorithmic"] = res["hbm_bytes_per_launch"] / res["algorithmic_bytes_per_launch"]
         for name, p in (("fetch", fpath), ("write", wpath)):
             rows = [r for r in csv.DictReader(open(p)) if args.kernel in r["Kernel_Name"]]
-            with open(os.path.join(out_dir, f"{args.tag}_pmc_{name}_{args.mode}.csv"), "w", newline="") as f:
+            with open(os.path.join(out_dir, f"{args.tag}_pmc_{name}_{args.mode}{args.suffix}.csv"), "w", newline="") as f:
                 w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
                 w.writeheader()
                 w.writerows(rows)

@@ -132,6 +132,16 @@ constexpr ObsTable make_obs_table() {
 }
 
 __constant__ ObsTable kObsTab = make_obs_table();
+constexpr int kTabWords = 2 * 78;
+
+// The gather table is copied into LDS once per wave, at the start (before any store): a lane-
+// indexed read of the __constant__ table is a global_load, and on gfx9 vmcnt counts stores too, so
+// waiting for a table load issued between the stream's stores drains every store before it
+// (measured in the ISA: an s_waitcnt vmcnt(0) per unrolled stream iteration).  ds_read waits
+// on lgkmcnt instead, which the stores do not touch.
+__device__ __forceinline__ void stage_obs_table(uint32_t* tab, int lane) {
+  for (int i = lane; i < kTabWords; i += kWave) tab[i] = kObsTab.w[i];
+}
 
 // ---- math (transcendental-free; identical op sequence in oracle/vss_oracle.c) ----------------
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
@@ -493,6 +503,10 @@ __device__ __forceinline__ void physics_split(Bodies& b, const float a[12]) {
   }
 }
 
+// s_waitcnt vmcnt(0) (expcnt / lgkmcnt untouched: 0x0F70 in gfx9's encoding), placed where only
+// loads are outstanding; the compiler's waitcnt pass sees the builtin and drops later waits.
+__device__ __forceinline__ void wait_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // ---- state I/O -----------------------------------------------------------------------------------
 __device__ __forceinline__ void load_bodies(const float* __restrict__ st, int64_t n, int64_t f, Bodies& b) {
   b.bx = st[VSS_CH_BALL_X * n + f]; b.by = st[VSS_CH_BALL_Y * n + f];
@@ -594,7 +608,8 @@ __device__ __forceinline__ void write_obs_record(float* rec, const Bodies& b, co
 // the last record and their stores predicated off).
 constexpr int kObsUnroll = 4;
 template <int A>
-__device__ __forceinline__ void coop_store_obs(float* __restrict__ out, int nv, const float* lds, int lane) {
+__device__ __forceinline__ void coop_store_obs(float* __restrict__ out, int nv, const float* lds, const uint32_t* tab,
+                                               int lane) {
   constexpr int Q = 13 * A;  // float4 per field
   constexpr int QD = kWave / Q, QR = kWave % Q;
   constexpr uint32_t RB = 4u * obs_rec<A>();  // record bytes
@@ -608,7 +623,7 @@ __device__ __forceinline__ void coop_store_obs(float* __restrict__ out, int nv, 
     float4 v[kObsUnroll];
 #pragma unroll
     for (int u = 0; u < kObsUnroll; ++u) {
-      const uint2 t = reinterpret_cast<const uint2*>(kObsTab.w)[j4];  // constant table (L1/K$-resident)
+      const uint2 t = reinterpret_cast<const uint2*>(tab)[j4];  // LDS copy of kObsTab (stage_obs_table)
       const uint32_t r = rb < rb_last ? rb : rb_last;
       v[u].x = *reinterpret_cast<const float*>(L + r + (t.x & 0xffffu));
       v[u].y = *reinterpret_cast<const float*>(L + r + (t.x >> 16));
@@ -827,7 +842,9 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   constexpr bool kSplit = 2 * kFpw <= kWave;
   constexpr int kLds = kSplit ? (32 * kRec > kFpw * obs_rec<A>() ? 32 * kRec : kFpw * obs_rec<A>()) : kWave * kRec;
   static_assert(kFpw * obs_rec<A>() <= kLds, "observation records must fit the LDS block");
-  __shared__ float lds[kLds];
+  __shared__ float lds[kLds + kTabWords];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(lds + kLds);
+  stage_obs_table(tab, threadIdx.x);
 
   const int64_t n = args.n;
   const int lane = threadIdx.x;
@@ -930,11 +947,16 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   float rew[24];
   const int64_t done = rewards_and_done(args.p, b, pbx, pby, prx, pry, a, progress, rew);
 
+  // Retire every load of this launch here, before the first store.  gfx9's vmcnt counts loads and
+  // stores in issue order, so a load still pending after the streams (the rng counter, first used
+  // by the reset) could only be waited for by draining the streams' stores with it.
+  wait_loads();
+
   // -- terminal observation (envs/vss.py:195-196) ----------------------------------------------------------
   if (lane < kFpw) write_obs_record<A>(orec, b, a);
   __syncthreads();
 #ifndef VSS_PROF_SKIP_OBS
-  coop_store_obs<A>(args.io.terminal_obs + f0 * (52 * A), nv, lds, lane);
+  coop_store_obs<A>(args.io.terminal_obs + f0 * (52 * A), nv, lds, tab, lane);
 #endif
   __syncthreads();
 
@@ -957,7 +979,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   if (lane < kFpw) write_obs_record<A>(orec, b, dof);
   __syncthreads();
 #ifndef VSS_PROF_SKIP_OBS
-  coop_store_obs<A>(args.io.obs + f0 * (52 * A), nv, lds, lane);
+  coop_store_obs<A>(args.io.obs + f0 * (52 * A), nv, lds, tab, lane);
 #endif
   __syncthreads();
 
@@ -1070,7 +1092,9 @@ __device__ __forceinline__ void stage12(const float4 pre[3], int nv, float* lds,
 
 __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
   static_assert(kFpwRollout * kRecObs6 <= kWave * kRec, "observation records must fit the LDS block");
-  __shared__ float lds[kWave * kRec];
+  __shared__ float lds[kWave * kRec + kTabWords];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(lds + kWave * kRec);
+  stage_obs_table(tab, threadIdx.x);
   const int64_t n = args.n;
   const int lane = threadIdx.x;
   constexpr bool kSplit = 2 * kFpwRollout == kWave;  // lanes L and L + 32 hold the same field
@@ -1122,9 +1146,13 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
     float rew[24];
     done = rewards_and_done(args.p, b, pbx, pby, prx, pry, a, progress, rew);
 
+    // the next step's action prefetch (issued before this step's physics) is retired here, before
+    // this step's stores: the previous step's stores, issued before it, have drained behind the
+    // physics, and the streams below leave no load pending (see wait_loads)
+    wait_loads();
     if (lane < kFpwRollout) write_obs_record<6>(orec, b, a);
     __syncthreads();
-    coop_store_obs<6>(args.io.terminal_obs + (step_off + f0) * 312, nv, lds, lane);
+    coop_store_obs<6>(args.io.terminal_obs + (step_off + f0) * 312, nv, lds, tab, lane);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 12; ++i) dof[i] = a[i];
@@ -1137,7 +1165,7 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
     }
     if (lane < kFpwRollout) write_obs_record<6>(orec, b, dof);
     __syncthreads();
-    coop_store_obs<6>(args.io.obs + (step_off + f0) * 312, nv, lds, lane);
+    coop_store_obs<6>(args.io.obs + (step_off + f0) * 312, nv, lds, tab, lane);
     __syncthreads();
     if (writer) {
 #pragma unroll
@@ -1190,7 +1218,9 @@ __global__ __launch_bounds__(kWave) void reset_kernel(int64_t n, vss_params p, v
 
 template <int A>
 __global__ __launch_bounds__(kWave) void observe_kernel(int64_t n, vss_state s, float* obs) {
-  __shared__ float lds[kWave * obs_rec<A>()];
+  __shared__ float lds[kWave * obs_rec<A>() + kTabWords];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(lds + kWave * obs_rec<A>());
+  stage_obs_table(tab, threadIdx.x);
   const int lane = threadIdx.x;
   const int64_t f0 = (int64_t)blockIdx.x * kWave;
   const int nv = (int)(n - f0 < kWave ? n - f0 : kWave);
@@ -1208,8 +1238,9 @@ __global__ __launch_bounds__(kWave) void observe_kernel(int64_t n, vss_state s, 
     load_bodies(s.state, n, f, b);
     write_obs_record<A>(orec, b, dof);
   }
+  wait_loads();
   __syncthreads();
-  coop_store_obs<A>(obs + f0 * (52 * A), nv, lds, lane);
+  coop_store_obs<A>(obs + f0 * (52 * A), nv, lds, tab, lane);
 }
 
 // RecordEpisodeStatisticsTorch.step (envs/wrappers.py:66-87), one row per lane.  The products

@@ -152,6 +152,9 @@ namespace vgemm {
 #ifndef VSS_LT_PROBE
 #define VSS_LT_PROBE 0
 #endif
+#ifndef VSS_LT_PRIO
+#define VSS_LT_PRIO 0  // 1: gemm_kernel_d2 raises the wave priority over its MFMA phases
+#endif
 #ifndef VSS_LT_EXACT
 #define VSS_LT_EXACT 1  // unmasked loads for exact shapes
 #endif
@@ -439,6 +442,144 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(Gemm
   }
 }
 
+// Exact shapes (rows % BM == 0, K % 64 == 0), loads TWO K tiles ahead (VSS_LT_DEPTH == 2): two
+// register sets alternate with the two LDS buffers, so a K tile's global loads are issued two MFMA
+// phases before the LDS write that consumes them (one phase in gemm_kernel: the HBM-missing A rows
+// of a new row band then stall that write, and through the barrier every wave of the block).  K
+// tile g of the block's flat sequence (its tiles' K tiles back to back): MFMAs on LDS[g & 1];
+// write R[(g + 1) & 1] (= K tile g + 1) into LDS[(g + 1) & 1]; barrier; load K tile g + 3 into
+// R[(g + 1) & 1].  The fetch cursor advances its pointers by one K tile (32 floats) per load and
+// recomputes them only at a tile change.
+template <int EPI, class C>
+__global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel_d2(GemmArgs p) {
+  constexpr int BM = C::BM, BN = C::BN, TM = C::TM, TN = C::TN, LROWS = C::LROWS, RA = C::RA, RB = C::RB;
+  __shared__ float lds[C::LDSF];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv / C::WN, wn = wv % C::WN;
+  const int nb = p.n / BN;
+  const int K = p.k, ktiles = K / kKS;  // even (K % 64 == 0)
+  const int G = gridDim.x, tiles = (int)p.tiles;
+  const int slot = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  if (slot >= tiles) return;
+
+  const int lr = tid >> 3, lc = (tid & 7) * 4;
+  const int64_t KL = (int64_t)LROWS * K;
+  // fetch cursor: the next K tile to load (tile f_tile, k tile f_kt); past the last tile it keeps
+  // re-loading the last one (in bounds, never multiplied)
+  int f_tile = slot, f_kt = 0;
+  const float* fa;
+  const float* fb;
+  auto point = [&](int t) {
+    fa = p.a + ((int64_t)(t / nb) * BM + lr) * K + lc;
+    fb = p.b + ((int64_t)((t % nb) * BN) + lr) * K + lc;
+  };
+  point(f_tile);
+  auto advance = [&]() {
+    if (++f_kt < ktiles) {
+      fa += kKS;
+      fb += kKS;
+    } else if (f_tile + G < tiles) {
+      f_kt = 0;
+      f_tile += G;
+      point(f_tile);
+    } else {
+      f_kt = ktiles - 1;  // stay on the block's last K tile
+    }
+  };
+  auto gload = [&](float4 (&ra)[RA], float4 (&rb)[RB]) {
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      const vupd::f32x4 v = *reinterpret_cast<const vupd::f32x4*>(fa + i * KL);
+      ra[i] = make_float4(v.x, v.y, v.z, v.w);
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const vupd::f32x4 v = *reinterpret_cast<const vupd::f32x4*>(fb + i * KL);
+      rb[i] = make_float4(v.x, v.y, v.z, v.w);
+    }
+    advance();
+  };
+  auto swrite = [&](const float4 (&ra)[RA], const float4 (&rb)[RB], int buf) {
+    float* As = lds + buf * (BM + BN) * kLS;
+    float* Bs = As + BM * kLS;
+#pragma unroll
+    for (int i = 0; i < RA; ++i) *reinterpret_cast<float4*>(As + (lr + LROWS * i) * kLS + lc) = ra[i];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) *reinterpret_cast<float4*>(Bs + (lr + LROWS * i) * kLS + lc) = rb[i];
+  };
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 acc[TM][TN];
+  auto mfma_tile = [&](int buf) {
+#if VSS_LT_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
+    const float* As = lds + buf * (BM + BN) * kLS + (wm * C::WROWS + r) * kLS + h * 16;
+    const float* Bs = lds + buf * (BM + BN) * kLS + BM * kLS + (wn * C::WCOLS + r) * kLS + h * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 a4[TM], b4[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a4[i] = *reinterpret_cast<const float4*>(As + i * 32 * kLS + q * 4);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b4[j] = *reinterpret_cast<const float4*>(Bs + j * 32 * kLS + q * 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const float av = s == 0 ? a4[i].x : s == 1 ? a4[i].y : s == 2 ? a4[i].z : a4[i].w;
+            const float bv = s == 0 ? b4[j].x : s == 1 ? b4[j].y : s == 2 ? b4[j].z : b4[j].w;
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+          }
+    }
+#if VSS_LT_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+  };
+
+  float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 ra0[RA], rb0[RB], ra1[RA], rb1[RB];
+  gload(ra0, rb0);  // K tile 0
+  swrite(ra0, rb0, 0);
+  gload(ra1, rb1);  // K tile 1
+  gload(ra0, rb0);  // K tile 2
+  __syncthreads();
+  int tile = slot;
+  for (;;) {
+    const int next = tile + G;
+    const bool has_next = next < tiles;
+    const int64_t row0 = (int64_t)(tile / nb) * BM;
+    const int col0 = (tile % nb) * BN;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = (f32x16){0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // K tiles in pairs: even g (LDS 0, writes R1 -> LDS 1, reloads R1), odd g (LDS 1, R0 -> LDS 0)
+    for (int kt = 0; kt < ktiles; kt += 2) {
+      mfma_tile(0);
+      swrite(ra1, rb1, 1);
+      __syncthreads();
+      gload(ra1, rb1);
+      mfma_tile(1);
+      swrite(ra0, rb0, 0);
+      __syncthreads();
+      gload(ra0, rb0);
+    }
+    // epilogue through LDS buffer 1: every wave has passed the barrier after its last read of it,
+    // and the next tile's first K tile sits in LDS 0
+    store_tile<EPI, TM, TN>(p, acc, lds + (BM + BN) * kLS + wv * (32 * kES), row0 + wm * C::WROWS,
+                            col0 + wn * C::WCOLS, csum);
+    if (!has_next) break;
+    __syncthreads();  // the next tile's second K tile is written into LDS 1 (the scratch)
+    tile = next;
+  }
+  if constexpr (EPI == EPI_DTANH) {
+    __syncthreads();
+    write_colsums<C::WM, BN>(p, csum, lds, slot, nb, wm, wn * C::WCOLS);
+  }
+}
+
 // The persistent grid is sized for MI355X (256 CUs) on every device: a block walks its tiles however
 // many blocks are resident, so the grid -- and with it the bias-gradient partial layout and its
 // summation order -- does not depend on the device the call runs on.
@@ -485,9 +626,17 @@ static bool shape_ok(int64_t rows, int32_t k, int32_t n) {
          n <= 65536 && (rows + 127) / 128 * (n / 128) <= 0x7fff0000;  // tile + grid stays in int
 }
 
+#ifndef VSS_LT_DEPTH
+#define VSS_LT_DEPTH 2  // 2: exact shapes with K % 64 == 0 on 128 x 128 blocks load two K tiles ahead
+#endif
+
 template <int EPI, bool EXACT>
 static void launch_kind(const GemmArgs& a, const Plan& pl, hipStream_t s) {
   const dim3 grid((unsigned)pl.grid);
+  if (VSS_LT_DEPTH == 2 && EXACT && pl.kind == 0 && a.k % (2 * kKS) == 0) {
+    hipLaunchKernelGGL((gemm_kernel_d2<EPI, Cfg128>), grid, dim3(Cfg128::THREADS), 0, s, a);
+    return;
+  }
   if (pl.kind == 1)
     hipLaunchKernelGGL((gemm_kernel<EPI, Cfg256, EXACT>), grid, dim3(Cfg256::THREADS), 0, s, a);
   else

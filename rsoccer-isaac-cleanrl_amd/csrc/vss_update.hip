@@ -152,6 +152,12 @@ namespace vgemm {
 #ifndef VSS_LT_PROBE
 #define VSS_LT_PROBE 0
 #endif
+#ifndef VSS_LT_DEPTH
+#define VSS_LT_DEPTH 2  // 2: exact shapes with K % 64 == 0 on 128 x 128 blocks load two K tiles ahead
+#endif
+#ifndef VSS_LT_D2CFG
+#define VSS_LT_D2CFG 256  // 256: the forward's exact shapes with n % 256 == 0 run gemm_kernel_d2 on 256 x 256 blocks
+#endif
 #ifndef VSS_LT_PRIO
 #define VSS_LT_PRIO 0  // 1: gemm_kernel_d2 raises the wave priority over its MFMA phases
 #endif
@@ -596,13 +602,19 @@ struct Plan {
   int64_t tiles, grid;
 };
 
-static Plan plan(int64_t rows, int32_t k, int32_t n) {
+static Plan plan(int64_t rows, int32_t k, int32_t n, bool forward) {
   Plan pl;
   // Exact shapes (rows % 128 == 0, K % 32 == 0: the update's layers but the first) run the
   // 128 x 128 blocks with unmasked, pipelined loads (fastest there); the masked form is fastest on
   // 256 x 256 blocks (profiles/r01_gemm_fused_bench.log).
   const bool exact = VSS_LT_EXACT && rows % Cfg128::BM == 0 && k % kKS == 0;
   pl.kind = (VSS_LT_CFG == 256 && !exact && n % 256 == 0) ? 1 : 0;
+  // the forward's exact shapes on 256 x 256 blocks with the two-deep pipeline: 123-134 TF vs 116-127 on
+  // 128 x 128 (profiles/r02_gemm_d2c256.log); the backward's epilogue needs more registers than a
+  // 256 x 256 block leaves (it spills), so it stays on 128 x 128
+  if (VSS_LT_D2CFG == 256 && VSS_LT_DEPTH == 2 && forward && exact && rows % Cfg256::BM == 0 && k % (2 * kKS) == 0 &&
+      n % 256 == 0)
+    pl.kind = 1;
   static const int BMs[2] = {Cfg128::BM, Cfg256::BM};
   static const int BNs[2] = {Cfg128::BN, Cfg256::BN};
   static const int BPC[2] = {Cfg128::BLOCKS_PER_CU, Cfg256::BLOCKS_PER_CU};
@@ -626,15 +638,16 @@ static bool shape_ok(int64_t rows, int32_t k, int32_t n) {
          n <= 65536 && (rows + 127) / 128 * (n / 128) <= 0x7fff0000;  // tile + grid stays in int
 }
 
-#ifndef VSS_LT_DEPTH
-#define VSS_LT_DEPTH 2  // 2: exact shapes with K % 64 == 0 on 128 x 128 blocks load two K tiles ahead
-#endif
 
 template <int EPI, bool EXACT>
 static void launch_kind(const GemmArgs& a, const Plan& pl, hipStream_t s) {
   const dim3 grid((unsigned)pl.grid);
   if (VSS_LT_DEPTH == 2 && EXACT && pl.kind == 0 && a.k % (2 * kKS) == 0) {
     hipLaunchKernelGGL((gemm_kernel_d2<EPI, Cfg128>), grid, dim3(Cfg128::THREADS), 0, s, a);
+    return;
+  }
+  if (VSS_LT_D2CFG == 256 && VSS_LT_DEPTH == 2 && EPI == EPI_TANH && EXACT && pl.kind == 1 && a.k % (2 * kKS) == 0) {
+    hipLaunchKernelGGL((gemm_kernel_d2<EPI_TANH, Cfg256>), grid, dim3(Cfg256::THREADS), 0, s, a);
     return;
   }
   if (pl.kind == 1)
@@ -699,13 +712,13 @@ int vss_linear_tanh(void* stream, int64_t rows, int32_t k_in, int32_t n_out, con
     return VSS_E_ARG;
   if (rows == 0) return VSS_OK;
   const vgemm::GemmArgs a{rows, n_out, k_in, x, w, bias, nullptr, y, nullptr, 0};
-  return vgemm::launch<vgemm::EPI_TANH>(stream, a, vgemm::plan(rows, k_in, n_out));
+  return vgemm::launch<vgemm::EPI_TANH>(stream, a, vgemm::plan(rows, k_in, n_out, true));
 }
 
 int64_t vss_linear_tanh_backward_chunks(int64_t rows, int32_t k_next, int32_t n_out) {
   if (!vgemm::shape_ok(rows, k_next, n_out)) return -1;
   if (rows == 0) return 0;
-  const vgemm::Plan pl = vgemm::plan(rows, k_next, n_out);
+  const vgemm::Plan pl = vgemm::plan(rows, k_next, n_out, false);
   return pl.grid / (n_out / pl.bn);
 }
 
@@ -716,7 +729,7 @@ int vss_linear_tanh_backward(void* stream, int64_t rows, int32_t k_next, int32_t
     return VSS_E_ARG;
   if (rows == 0) return VSS_OK;
   const vgemm::GemmArgs a{rows, n_out, k_next, grad_next, w_next_t, nullptr, y, grad_in, bias_partial, 0};
-  return vgemm::launch<vgemm::EPI_DTANH>(stream, a, vgemm::plan(rows, k_next, n_out));
+  return vgemm::launch<vgemm::EPI_DTANH>(stream, a, vgemm::plan(rows, k_next, n_out, false));
 }
 
 }  // extern "C"

@@ -43,6 +43,19 @@ constexpr int kWave = 64;
 #ifndef VSS_FPW_DMA
 #define VSS_FPW_DMA 32
 #endif
+// Persistent step kernel (profiling knob, off in the product): at most VSS_STEP_GRID waves, each
+// walking batches w, w + G, ... with the next batch's inputs loaded during this batch's compute.
+// Measured at 65,536 fields (profiles/r02_ablate_persist_*.log): 1,024 waves x 2 batches is 12-33 %
+// SLOWER than 2,048 waves x 1 batch (FULL 45.3 vs 39.4 us, SA 33.2 vs 24.5 us): the second wave per
+// SIMD hides the load -> physics -> store latency chain better than in-wave prefetching does, and
+// on gfx9 a wave cannot consume a load issued after its previous stores without draining them.
+#ifndef VSS_STEP_PERSIST
+#define VSS_STEP_PERSIST 0
+#endif
+#ifndef VSS_STEP_GRID
+#define VSS_STEP_GRID 1024
+#endif
+constexpr bool kStepPersist = VSS_STEP_PERSIST != 0;
 template <int MODE>
 constexpr int fields_per_wave() {
   return MODE == VSS_MODE_FULL ? VSS_FPW_FULL
@@ -818,257 +831,6 @@ __device__ __forceinline__ int64_t rewards_and_done(const vss_params& p, const B
   return (is_goal || progress >= (int64_t)p.max_episode_length) ? 1 : 0;
 }
 
-// ---- the step kernel -------------------------------------------------------------------------------
-struct StepArgs {
-  int64_t n;
-  vss_params p;
-  vss_state s;
-  vss_step_io io;
-  vss_replay_draws rd;  // REPLAY instantiations only (vss_step_replay)
-  uint32_t rd_rounds;   // rejection rounds one replay row holds
-};
-
-// REPLAY = false: the product kernel (Philox draws).  REPLAY = true: the parity entry
-// vss_step_replay, the same kernel consuming recorded reference draws (ResetDraws above; OU
-// normals from rd.normals) -- every other instruction is shared.
-template <int MODE, bool REPLAY = false>
-__global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
-  constexpr int A = MODE == VSS_MODE_FULL ? 6 : (MODE == VSS_MODE_DMA ? 3 : 1);
-  constexpr int R = MODE == VSS_MODE_DMA ? 3 : 1;
-  constexpr int NL = MODE == VSS_MODE_SA ? 2 : 6;  // learner action floats per field
-  constexpr int kFpw = fields_per_wave<MODE>();
-  // <= 32 fields per wave: lanes L and L + 32 hold field L (physics_split); lanes < 32 address the
-  // LDS records, so LDS holds 32 plain records or kFpw observation records, whichever is larger
-  constexpr bool kSplit = 2 * kFpw <= kWave;
-  constexpr int kLds = kSplit ? (32 * kRec > kFpw * obs_rec<A>() ? 32 * kRec : kFpw * obs_rec<A>()) : kWave * kRec;
-  static_assert(kFpw * obs_rec<A>() <= kLds, "observation records must fit the LDS block");
-  __shared__ float lds[kLds + kTabWords];
-  uint32_t* tab = reinterpret_cast<uint32_t*>(lds + kLds);
-  stage_obs_table(tab, threadIdx.x);
-
-  const int64_t n = args.n;
-  const int lane = threadIdx.x;
-  const int fl = kSplit ? (lane & 31) : lane;  // this lane's field within the wave
-  const int64_t f0 = (int64_t)blockIdx.x * kFpw;
-  const int nv = (int)(n - f0 < kFpw ? n - f0 : kFpw);
-  const int64_t f = f0 + fl;
-  const bool valid = fl < nv;
-  const bool owner = valid && (!kSplit || lane < 32);  // stores the field's outputs
-  const bool writer = !kSplit || lane < 32;            // writes the field's LDS record slots
-  const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
-  float* rec = lds + fl * kRec;
-  float* orec = lds + lane * obs_rec<A>();  // observation record (lanes < kFpw)
-
-  // -- state loads first (46 coalesced channel loads in flight), then the action transpose -------
-  int64_t progress = 0, reset_prev = 0;
-  uint32_t ctr = 0;
-  Bodies b = {};
-  if (valid) {
-    progress = args.s.progress_buf[f];
-    reset_prev = args.s.reset_buf[f];
-    ctr = args.s.rng_counter[f];
-    load_bodies(args.s.state, n, f, b);
-  }
-
-  // -- actions: FULL reads (N,12); wrapped modes read + update the OU action buffer --------------
-  float a[12];
-  if constexpr (MODE == VSS_MODE_FULL) {
-    coop_load<12>(args.io.actions + f0 * 12, nv, lds, lane);
-  } else {
-    coop_load<12>(args.io.ou_buf + f0 * 12, nv, lds, lane);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 12; ++k) a[k] = rec[k];
-  __syncthreads();
-
-  if constexpr (MODE != VSS_MODE_FULL) {
-    // random_ou (envs/wrappers.py:5-19): a <- clamp(a - 0.1 a + N(0, 0.15^2), -1, 1); the learner
-    // slots (pairs 0 for SA, 0..2 for CMA/DMA) are overwritten, so their normals are not needed.
-    constexpr int first_block = MODE == VSS_MODE_SA ? 0 : 1;
-    if constexpr (REPLAY) {
-      // torch.normal(0, 0.15, (N, 2, 3, 2)) of random_ou: the field's 12 recorded samples
-      if (valid) {
-        const float* z = args.rd.normals + f * 12;
-#pragma unroll
-        for (int k = NL; k < 12; ++k) a[k] = clampf((a[k] - K_OU_THETA * a[k]) + z[k], -1.0f, 1.0f);
-      }
-    } else {
-#pragma unroll
-      for (int blk = first_block; blk < 3; ++blk) {
-        uint32_t o[4];
-        philox(k0, k1, (uint32_t)f, ctr, kPurposeOU << 24, (uint32_t)blk, o);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          int k = 4 * blk + 2 * h;
-          if (k < NL) continue;
-          float u1 = u01_open0(o[2 * h]);
-          float u2 = u01(o[2 * h + 1]);
-          float rad = sqrtf(-2.0f * logf_poly(u1));
-          float sz, cz;
-          sincos_turn(u2, sz, cz);
-          a[k] = clampf((a[k] - K_OU_THETA * a[k]) + K_OU_SIGMA * (rad * cz), -1.0f, 1.0f);
-          a[k + 1] = clampf((a[k + 1] - K_OU_THETA * a[k + 1]) + K_OU_SIGMA * (rad * sz), -1.0f, 1.0f);
-        }
-      }
-    }
-    coop_load<NL>(args.io.actions + f0 * NL, nv, lds, lane);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NL; ++k) a[k] = rec[k];
-    __syncthreads();
-  }
-  float ou[12];
-  if constexpr (MODE != VSS_MODE_FULL) {
-#pragma unroll
-    for (int k = 0; k < 12; ++k) ou[k] = a[k];
-  }
-
-  // -- Ext VecTask.step clamp + pre_physics_step (envs/vss.py:180-187) -----------------------------
-  const float clip = args.p.clip_actions;
-#pragma unroll
-  for (int k = 0; k < 12; ++k) a[k] = clampf(a[k], -clip, clip);
-  if (reset_prev != 0) progress = 0;
-
-  float pbx = b.bx, pby = b.by, prx[6], pry[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) { prx[i] = b.x[i]; pry[i] = b.y[i]; }
-
-  // -- gym.simulate replacement ------------------------------------------------------------------------
-#ifndef VSS_PROF_SKIP_PHYSICS  // profiling-only ablation knobs (tools/ablate.py); never set in the product
-  if (valid) {
-    if constexpr (kSplit) physics_split(b, a);
-    else physics(b, a);
-  }
-#endif
-
-  // -- post_physics_step: progress, rewards, dones (envs/vss.py:189-265) ----------------------------------
-  progress += 1;
-  float rew[24];
-  const int64_t done = rewards_and_done(args.p, b, pbx, pby, prx, pry, a, progress, rew);
-
-  // Retire every load of this launch here, before the first store.  gfx9's vmcnt counts loads and
-  // stores in issue order, so a load still pending after the streams (the rng counter, first used
-  // by the reset) could only be waited for by draining the streams' stores with it.
-  wait_loads();
-
-  // -- terminal observation (envs/vss.py:195-196) ----------------------------------------------------------
-  if (lane < kFpw) write_obs_record<A>(orec, b, a);
-  __syncthreads();
-#ifndef VSS_PROF_SKIP_OBS
-  coop_store_obs<A>(args.io.terminal_obs + f0 * (52 * A), nv, lds, tab, lane);
-#endif
-  __syncthreads();
-
-  // -- reset_dones (envs/vss.py:202, 267-333) ---------------------------------------------------------------
-  float dof[12];
-#pragma unroll
-  for (int k = 0; k < 12; ++k) dof[k] = a[k];
-#ifndef VSS_PROF_SKIP_RESET
-  if (valid && done) {
-    const ResetDraws rd{k0, k1, (uint32_t)f, ctr, 0u, REPLAY ? args.rd.uniforms + f * args.rd.uniform_stride : nullptr,
-                        REPLAY ? args.rd_rounds : (uint32_t)kMaxRejectRounds};
-    if constexpr (kSplit) reset_field_split<REPLAY>(b, rd);
-    else reset_field<REPLAY>(b, rd);
-#pragma unroll
-    for (int k = 0; k < 12; ++k) dof[k] = dof[k] * 0.0f;
-  }
-#endif
-
-  // -- observation after reset (envs/vss.py:203) -------------------------------------------------------------
-  if (lane < kFpw) write_obs_record<A>(orec, b, dof);
-  __syncthreads();
-#ifndef VSS_PROF_SKIP_OBS
-  coop_store_obs<A>(args.io.obs + f0 * (52 * A), nv, lds, tab, lane);
-#endif
-  __syncthreads();
-
-  // -- bookkeeping --------------------------------------------------------------------------------------------
-  const uint8_t time_out = (progress >= (int64_t)args.p.max_episode_length - 1) && done != 0;
-  if (owner) {
-    store_bodies(args.s.state, n, f, b);
-    args.s.progress_buf[f] = progress;
-    args.s.reset_buf[f] = done;
-    args.s.rng_counter[f] = ctr + 1u;
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      args.io.time_outs[f * R + k] = time_out;
-      args.io.progress_f[f * R + k] = (float)progress;
-    }
-    if constexpr (MODE == VSS_MODE_DMA) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) args.io.dones_rep[f * 3 + k] = done;
-    }
-  }
-
-  // dof_velocity_buf (N,12) and, wrapped, the OU action buffer (zeroed for done fields)
-  if (writer) {
-#pragma unroll
-    for (int k = 0; k < 12; ++k) rec[k] = dof[k];
-  }
-  __syncthreads();
-  coop_store<12>(args.s.dof_velocity_buf + f0 * 12, nv, lds, lane);
-  __syncthreads();
-  if constexpr (MODE != VSS_MODE_FULL) {
-    if (writer) {
-#pragma unroll
-      for (int k = 0; k < 12; ++k) rec[k] = done ? ou[k] * 0.0f : ou[k];
-    }
-    __syncthreads();
-    coop_store<12>(args.io.ou_buf + f0 * 12, nv, lds, lane);
-    __syncthreads();
-  }
-
-  // rewards
-  if constexpr (MODE == VSS_MODE_FULL) {
-    if (writer) {
-#pragma unroll
-      for (int k = 0; k < 24; ++k) rec[k] = rew[k];
-    }
-    __syncthreads();
-    coop_store<24>(args.io.rew + f0 * 24, nv, lds, lane);
-    if (owner && args.io.reward_sum) args.io.reward_sum[f] = ((rew[0] + rew[1]) + rew[2]) + rew[3];
-  } else if constexpr (MODE == VSS_MODE_SA) {
-    if (owner) {
-      reinterpret_cast<float4*>(args.io.rew)[f] = make_float4(rew[0], rew[1], rew[2], rew[3]);
-      args.io.reward_sum[f] = ((rew[0] + rew[1]) + rew[2]) + rew[3];
-    }
-  } else if constexpr (MODE == VSS_MODE_CMA) {
-    if (owner) {
-      float m[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) m[c] = ((rew[c] + rew[4 + c]) + rew[8 + c]) / 3.0f;
-      reinterpret_cast<float4*>(args.io.rew)[f] = make_float4(m[0], m[1], m[2], m[3]);
-      args.io.reward_sum[f] = ((m[0] + m[1]) + m[2]) + m[3];
-    }
-  } else {
-    if (writer) {
-#pragma unroll
-      for (int k = 0; k < 12; ++k) rec[k] = rew[k];
-    }
-    __syncthreads();
-    coop_store<12>(args.io.rew + f0 * 12, nv, lds, lane);
-    if (owner) {
-#pragma unroll
-      for (int ag = 0; ag < 3; ++ag)
-        args.io.reward_sum[f * 3 + ag] = ((rew[4 * ag] + rew[4 * ag + 1]) + rew[4 * ag + 2]) + rew[4 * ag + 3];
-    }
-  }
-}
-
-// ---- K control steps per launch (open-loop action sequences) -----------------------------------------
-// Same per-step semantics as K consecutive step_kernel<FULL> launches, bit for bit (the Philox
-// counter of step k is rng_counter + k), but the field state stays in registers across steps, each
-// step's observation stores drain while the next step's physics runs, and the next step's actions
-// are prefetched into registers before the current step's streams are issued.
-struct RolloutArgs {
-  int64_t n;
-  int32_t k_steps;
-  vss_params p;
-  vss_state s;
-  vss_rollout_io io;
-};
-
 __device__ __forceinline__ void prefetch12(const float* __restrict__ g, int nv, int lane, float4 pre[3]) {
   const float4* g4 = reinterpret_cast<const float4*>(g);
 #pragma unroll
@@ -1089,6 +851,325 @@ __device__ __forceinline__ void stage12(const float4 pre[3], int nv, float* lds,
     }
   }
 }
+
+// The learner action rows (nv, NL) of a wrapped-mode batch as float2 pieces (8-B aligned per the
+// ABI), prefetched into registers and later staged into the LDS record layout like stage12.
+template <int NL>
+__device__ __forceinline__ void prefetch_lrn(const float* __restrict__ g, int nv, int lane, float2 pre[2]) {
+  const float2* g2 = reinterpret_cast<const float2*>(g);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int q = lane + j * kWave;
+    if (q < nv * NL / 2) pre[j] = g2[q];
+  }
+}
+
+template <int NL>
+__device__ __forceinline__ void stage_lrn(const float2 pre[2], int nv, float* lds, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int q = lane + j * kWave;
+    if (q < nv * NL / 2) {
+      const int e = q * 2, fl = e / NL, k = e - fl * NL;
+      float* d = lds + fl * kRec + k;
+      d[0] = pre[j].x; d[1] = pre[j].y;
+    }
+  }
+}
+
+// ---- the step kernel -------------------------------------------------------------------------------
+// One batch's inputs (kFpw fields of one wave), loaded into registers one batch ahead: the field's
+// bookkeeping and 46 live state channels, and the wave's contiguous AoS blocks of the batch's
+// 12-float action rows (FULL) or OU buffer rows (wrapped) and learner action rows (wrapped).
+struct BatchIn {
+  int64_t progress, reset_prev;
+  uint32_t ctr;
+  Bodies b;
+  float4 blk[3];  // (nv, 12) block: float4 q = lane + 64 j, q < 3 nv
+  float2 lrn[2];  // (nv, NL) block: float2 q = lane + 64 j, q < nv NL / 2
+};
+
+struct StepArgs {
+  int64_t n;
+  vss_params p;
+  vss_state s;
+  vss_step_io io;
+  vss_replay_draws rd;  // REPLAY instantiations only (vss_step_replay)
+  uint32_t rd_rounds;   // rejection rounds one replay row holds
+};
+
+// REPLAY = false: the product kernel (Philox draws).  REPLAY = true: the parity entry
+// vss_step_replay, the same kernel consuming recorded reference draws (ResetDraws above; OU
+// normals from rd.normals) -- every other instruction is shared.
+template <int MODE>
+__device__ __forceinline__ void load_batch(const StepArgs& args, int64_t f0, int nv, int fl, int lane, BatchIn& in) {
+  constexpr int NL = MODE == VSS_MODE_SA ? 2 : 6;
+  const int64_t f = f0 + fl;
+  in.progress = 0;
+  in.reset_prev = 0;
+  in.ctr = 0;
+  in.b = {};
+  if (fl < nv) {
+    in.progress = args.s.progress_buf[f];
+    in.reset_prev = args.s.reset_buf[f];
+    in.ctr = args.s.rng_counter[f];
+    load_bodies(args.s.state, args.n, f, in.b);
+  }
+  prefetch12((MODE == VSS_MODE_FULL ? args.io.actions : args.io.ou_buf) + f0 * 12, nv, lane, in.blk);
+  if constexpr (MODE != VSS_MODE_FULL) prefetch_lrn<NL>(args.io.actions + f0 * NL, nv, lane, in.lrn);
+}
+
+template <int MODE, bool REPLAY = false>
+__global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
+  constexpr int A = MODE == VSS_MODE_FULL ? 6 : (MODE == VSS_MODE_DMA ? 3 : 1);
+  constexpr int R = MODE == VSS_MODE_DMA ? 3 : 1;
+  constexpr int NL = MODE == VSS_MODE_SA ? 2 : 6;  // learner action floats per field
+  constexpr int kFpw = fields_per_wave<MODE>();
+  // <= 32 fields per wave: lanes L and L + 32 hold field L (physics_split); lanes < 32 address the
+  // LDS records, so LDS holds 32 plain records or kFpw observation records, whichever is larger
+  constexpr bool kSplit = 2 * kFpw <= kWave;
+  constexpr int kLds = kSplit ? (32 * kRec > kFpw * obs_rec<A>() ? 32 * kRec : kFpw * obs_rec<A>()) : kWave * kRec;
+  static_assert(kFpw * obs_rec<A>() <= kLds, "observation records must fit the LDS block");
+  __shared__ float lds[kLds + kTabWords];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(lds + kLds);
+  stage_obs_table(tab, threadIdx.x);
+#ifdef VSS_PROF_STAGGER  // profiling knob: odd waves start VSS_PROF_STAGGER x 64 x 64 cycles late
+  if (blockIdx.x & 1)
+    for (int i = 0; i < VSS_PROF_STAGGER; ++i) __builtin_amdgcn_s_sleep(64);
+#endif
+
+  const int64_t n = args.n;
+  const int lane = threadIdx.x;
+  const int fl = kSplit ? (lane & 31) : lane;  // this lane's field within the wave
+  const bool writer = !kSplit || lane < 32;    // writes the field's LDS record slots
+  const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
+  float* rec = lds + fl * kRec;
+  float* orec = lds + lane * obs_rec<A>();  // observation record (lanes < kFpw)
+
+  // Persistent over batches of kFpw fields: wave w advances batches w, w + G, w + 2G, ... (G =
+  // gridDim.x, sized by the host).  A batch's inputs are loaded one batch ahead (BatchIn), so they
+  // land while the wave computes the batch before, and the previous batch's stores drain behind this
+  // batch's compute (both are retired by the wait_loads() before this batch's first store).
+  const int64_t nbt = (n + kFpw - 1) / kFpw;
+  auto batch_nv = [&](int64_t t) { return (int)(n - t * kFpw < kFpw ? n - t * kFpw : kFpw); };
+  int64_t bt = blockIdx.x;
+  BatchIn cur;
+  load_batch<MODE>(args, bt * kFpw, batch_nv(bt), fl, lane, cur);
+  for (;;) {
+    const int64_t f0 = bt * kFpw;
+    const int nv = batch_nv(bt);
+    const int64_t f = f0 + fl;
+    const bool valid = fl < nv;
+    const bool owner = valid && writer;  // stores the field's outputs
+    const int64_t btn = bt + gridDim.x;
+    const bool more = kStepPersist && btn < nbt;
+    BatchIn nxt;
+    if (more) load_batch<MODE>(args, btn * kFpw, batch_nv(btn), fl, lane, nxt);
+
+    int64_t progress = cur.progress, reset_prev = cur.reset_prev;
+    uint32_t ctr = cur.ctr;
+    Bodies b = cur.b;
+
+    // -- actions: FULL reads (N,12); wrapped modes read + update the OU action buffer --------------
+    float a[12];
+    stage12(cur.blk, nv, lds, lane);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 12; ++k) a[k] = rec[k];
+    __syncthreads();
+
+    if constexpr (MODE != VSS_MODE_FULL) {
+      // random_ou (envs/wrappers.py:5-19): a <- clamp(a - 0.1 a + N(0, 0.15^2), -1, 1); the learner
+      // slots (pairs 0 for SA, 0..2 for CMA/DMA) are overwritten, so their normals are not needed.
+      constexpr int first_block = MODE == VSS_MODE_SA ? 0 : 1;
+      if constexpr (REPLAY) {
+        // torch.normal(0, 0.15, (N, 2, 3, 2)) of random_ou: the field's 12 recorded samples
+        if (valid) {
+          const float* z = args.rd.normals + f * 12;
+#pragma unroll
+          for (int k = NL; k < 12; ++k) a[k] = clampf((a[k] - K_OU_THETA * a[k]) + z[k], -1.0f, 1.0f);
+        }
+      } else {
+#pragma unroll
+        for (int blk = first_block; blk < 3; ++blk) {
+          uint32_t o[4];
+          philox(k0, k1, (uint32_t)f, ctr, kPurposeOU << 24, (uint32_t)blk, o);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            int k = 4 * blk + 2 * h;
+            if (k < NL) continue;
+            float u1 = u01_open0(o[2 * h]);
+            float u2 = u01(o[2 * h + 1]);
+            float rad = sqrtf(-2.0f * logf_poly(u1));
+            float sz, cz;
+            sincos_turn(u2, sz, cz);
+            a[k] = clampf((a[k] - K_OU_THETA * a[k]) + K_OU_SIGMA * (rad * cz), -1.0f, 1.0f);
+            a[k + 1] = clampf((a[k + 1] - K_OU_THETA * a[k + 1]) + K_OU_SIGMA * (rad * sz), -1.0f, 1.0f);
+          }
+        }
+      }
+      stage_lrn<NL>(cur.lrn, nv, lds, lane);
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < NL; ++k) a[k] = rec[k];
+      __syncthreads();
+    }
+    float ou[12];
+    if constexpr (MODE != VSS_MODE_FULL) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) ou[k] = a[k];
+    }
+
+    // -- Ext VecTask.step clamp + pre_physics_step (envs/vss.py:180-187) -----------------------------
+    const float clip = args.p.clip_actions;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) a[k] = clampf(a[k], -clip, clip);
+    if (reset_prev != 0) progress = 0;
+
+    float pbx = b.bx, pby = b.by, prx[6], pry[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) { prx[i] = b.x[i]; pry[i] = b.y[i]; }
+
+    // -- gym.simulate replacement ------------------------------------------------------------------------
+#ifndef VSS_PROF_SKIP_PHYSICS  // profiling-only ablation knobs (tools/ablate.py); never set in the product
+    if (valid) {
+      if constexpr (kSplit) physics_split(b, a);
+      else physics(b, a);
+    }
+#endif
+
+    // -- post_physics_step: progress, rewards, dones (envs/vss.py:189-265) ----------------------------------
+    progress += 1;
+    float rew[24];
+    const int64_t done = rewards_and_done(args.p, b, pbx, pby, prx, pry, a, progress, rew);
+
+    // Retire every pending load here, before this batch's first store (the next batch's inputs, issued
+    // before this batch's compute, and so landed by now; the previous batch's stores drain with them):
+    // gfx9's vmcnt counts loads and stores, and the compiler can only wait for a load issued before
+    // stores by draining those stores too -- e.g. the rng counter, first used by the reset.
+    wait_loads();
+
+    // -- terminal observation (envs/vss.py:195-196) ----------------------------------------------------------
+    if (lane < kFpw) write_obs_record<A>(orec, b, a);
+    __syncthreads();
+#ifndef VSS_PROF_SKIP_OBS
+    coop_store_obs<A>(args.io.terminal_obs + f0 * (52 * A), nv, lds, tab, lane);
+#endif
+    __syncthreads();
+
+    // -- reset_dones (envs/vss.py:202, 267-333) ---------------------------------------------------------------
+    float dof[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) dof[k] = a[k];
+#ifndef VSS_PROF_SKIP_RESET
+    if (valid && done) {
+      const ResetDraws rd{k0, k1, (uint32_t)f, ctr, 0u, REPLAY ? args.rd.uniforms + f * args.rd.uniform_stride : nullptr,
+                          REPLAY ? args.rd_rounds : (uint32_t)kMaxRejectRounds};
+      if constexpr (kSplit) reset_field_split<REPLAY>(b, rd);
+      else reset_field<REPLAY>(b, rd);
+#pragma unroll
+      for (int k = 0; k < 12; ++k) dof[k] = dof[k] * 0.0f;
+    }
+#endif
+
+    // -- observation after reset (envs/vss.py:203) -------------------------------------------------------------
+    if (lane < kFpw) write_obs_record<A>(orec, b, dof);
+    __syncthreads();
+#ifndef VSS_PROF_SKIP_OBS
+    coop_store_obs<A>(args.io.obs + f0 * (52 * A), nv, lds, tab, lane);
+#endif
+    __syncthreads();
+
+    // -- bookkeeping --------------------------------------------------------------------------------------------
+    const uint8_t time_out = (progress >= (int64_t)args.p.max_episode_length - 1) && done != 0;
+    if (owner) {
+      store_bodies(args.s.state, n, f, b);
+      args.s.progress_buf[f] = progress;
+      args.s.reset_buf[f] = done;
+      args.s.rng_counter[f] = ctr + 1u;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        args.io.time_outs[f * R + k] = time_out;
+        args.io.progress_f[f * R + k] = (float)progress;
+      }
+      if constexpr (MODE == VSS_MODE_DMA) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) args.io.dones_rep[f * 3 + k] = done;
+      }
+    }
+
+    // dof_velocity_buf (N,12) and, wrapped, the OU action buffer (zeroed for done fields)
+    if (writer) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) rec[k] = dof[k];
+    }
+    __syncthreads();
+    coop_store<12>(args.s.dof_velocity_buf + f0 * 12, nv, lds, lane);
+    __syncthreads();
+    if constexpr (MODE != VSS_MODE_FULL) {
+      if (writer) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) rec[k] = done ? ou[k] * 0.0f : ou[k];
+      }
+      __syncthreads();
+      coop_store<12>(args.io.ou_buf + f0 * 12, nv, lds, lane);
+      __syncthreads();
+    }
+
+    // rewards
+    if constexpr (MODE == VSS_MODE_FULL) {
+      if (writer) {
+#pragma unroll
+        for (int k = 0; k < 24; ++k) rec[k] = rew[k];
+      }
+      __syncthreads();
+      coop_store<24>(args.io.rew + f0 * 24, nv, lds, lane);
+      if (owner && args.io.reward_sum) args.io.reward_sum[f] = ((rew[0] + rew[1]) + rew[2]) + rew[3];
+    } else if constexpr (MODE == VSS_MODE_SA) {
+      if (owner) {
+        reinterpret_cast<float4*>(args.io.rew)[f] = make_float4(rew[0], rew[1], rew[2], rew[3]);
+        args.io.reward_sum[f] = ((rew[0] + rew[1]) + rew[2]) + rew[3];
+      }
+    } else if constexpr (MODE == VSS_MODE_CMA) {
+      if (owner) {
+        float m[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) m[c] = ((rew[c] + rew[4 + c]) + rew[8 + c]) / 3.0f;
+        reinterpret_cast<float4*>(args.io.rew)[f] = make_float4(m[0], m[1], m[2], m[3]);
+        args.io.reward_sum[f] = ((m[0] + m[1]) + m[2]) + m[3];
+      }
+    } else {
+      if (writer) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) rec[k] = rew[k];
+      }
+      __syncthreads();
+      coop_store<12>(args.io.rew + f0 * 12, nv, lds, lane);
+      if (owner) {
+#pragma unroll
+        for (int ag = 0; ag < 3; ++ag)
+          args.io.reward_sum[f * 3 + ag] = ((rew[4 * ag] + rew[4 * ag + 1]) + rew[4 * ag + 2]) + rew[4 * ag + 3];
+      }
+    }
+    if (!more) break;
+    __syncthreads();  // the next batch's LDS staging follows this batch's last LDS reads
+    cur = nxt;
+    bt = btn;
+  }
+}
+
+// ---- K control steps per launch (open-loop action sequences) -----------------------------------------
+// Same per-step semantics as K consecutive step_kernel<FULL> launches, bit for bit (the Philox
+// counter of step k is rng_counter + k), but the field state stays in registers across steps, each
+// step's observation stores drain while the next step's physics runs, and the next step's actions
+// are prefetched into registers before the current step's streams are issued.
+struct RolloutArgs {
+  int64_t n;
+  int32_t k_steps;
+  vss_params p;
+  vss_state s;
+  vss_rollout_io io;
+};
 
 __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
   static_assert(kFpwRollout * kRecObs6 <= kWave * kRec, "observation records must fit the LDS block");
@@ -1310,7 +1391,8 @@ static int step_impl(void* stream, int64_t n, int32_t mode, const vss_params* p,
   const int fpw = mode == VSS_MODE_FULL ? vss::fields_per_wave<VSS_MODE_FULL>()
                   : mode == VSS_MODE_SA ? vss::fields_per_wave<VSS_MODE_SA>()
                   : mode == VSS_MODE_CMA ? vss::fields_per_wave<VSS_MODE_CMA>() : vss::fields_per_wave<VSS_MODE_DMA>();
-  const dim3 grid((unsigned)((n + fpw - 1) / fpw)), block(vss::kWave);
+  const int64_t batches = (n + fpw - 1) / fpw;
+  const dim3 grid((unsigned)(vss::kStepPersist && batches > VSS_STEP_GRID ? VSS_STEP_GRID : batches)), block(vss::kWave);
   hipStream_t s = (hipStream_t)stream;
   switch (mode) {
     case VSS_MODE_FULL: hipLaunchKernelGGL((vss::step_kernel<VSS_MODE_FULL, REPLAY>), grid, block, 0, s, args); break;

@@ -919,8 +919,13 @@ __device__ __forceinline__ void load_batch(const StepArgs& args, int64_t f0, int
   if constexpr (MODE != VSS_MODE_FULL) prefetch_lrn<NL>(args.io.actions + f0 * NL, nv, lane, in.lrn);
 }
 
+#ifdef VSS_STEP_WPE  // profiling knob: minimum waves per SIMD the register allocation must allow
+#define VSS_STEP_ATTR __attribute__((amdgpu_waves_per_eu(VSS_STEP_WPE)))
+#else
+#define VSS_STEP_ATTR
+#endif
 template <int MODE, bool REPLAY = false>
-__global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
+__global__ __launch_bounds__(kWave) VSS_STEP_ATTR void step_kernel(StepArgs args) {
   constexpr int A = MODE == VSS_MODE_FULL ? 6 : (MODE == VSS_MODE_DMA ? 3 : 1);
   constexpr int R = MODE == VSS_MODE_DMA ? 3 : 1;
   constexpr int NL = MODE == VSS_MODE_SA ? 2 : 6;  // learner action floats per field

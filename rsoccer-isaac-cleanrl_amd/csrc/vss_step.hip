@@ -877,6 +877,58 @@ __device__ __forceinline__ void stage_lrn(const float2 pre[2], int nv, float* ld
   }
 }
 
+// random_ou's normals for the wrapped modes with the field's two lane halves sharing the work
+// (physics_split's lane pairing): each half draws the Philox blocks and Box-Muller pairs of its
+// share of the opponent slots, and v_permlane32_swap gives every lane all of them.  SA (slots
+// 2-11: pairs from blocks 0.h1, 1.h0, 1.h1, 2.h0, 2.h1): the lower half takes blocks 0-1, the upper
+// block 2; CMA/DMA (slots 6-11: 1.h1, 2.h0, 2.h1): the lower half block 1, the upper block 2.  The
+// same operations per pair as the unsplit loop in step_kernel (bit-identical results), about a
+// third fewer VALU instructions per wave.
+__device__ __forceinline__ void box_muller(uint32_t w1, uint32_t w2, float& zc, float& zs) {
+  const float u1 = u01_open0(w1), u2 = u01(w2);
+  const float rad = sqrtf(-2.0f * logf_poly(u1));
+  float sz, cz;
+  sincos_turn(u2, sz, cz);
+  zc = K_OU_SIGMA * (rad * cz);
+  zs = K_OU_SIGMA * (rad * sz);
+}
+
+template <int MODE>
+__device__ __forceinline__ void ou_noise_split(float a[12], uint32_t k0, uint32_t k1, uint32_t field, uint32_t ctr) {
+  const bool up = threadIdx.x >= 32;
+  float z[12];
+  if constexpr (MODE == VSS_MODE_SA) {
+    uint32_t p[4], q[4];
+    philox(k0, k1, field, ctr, kPurposeOU << 24, up ? 2u : 0u, p);
+    philox(k0, k1, field, ctr, kPurposeOU << 24, up ? 2u : 1u, q);
+    float c0, s0, c1, s1, c2, s2;
+    box_muller(up ? p[0] : p[2], up ? p[1] : p[3], c0, s0);  // lower: slots 2,3   upper: 8,9
+    box_muller(up ? p[2] : q[0], up ? p[3] : q[1], c1, s1);  // lower: slots 4,5   upper: 10,11
+    box_muller(q[2], q[3], c2, s2);                          // lower: slots 6,7   (upper: unused)
+    exch(c0, z[2], z[8]);
+    exch(s0, z[3], z[9]);
+    exch(c1, z[4], z[10]);
+    exch(s1, z[5], z[11]);
+    float unused;
+    exch(c2, z[6], unused);
+    exch(s2, z[7], unused);
+  } else {
+    uint32_t p[4];
+    philox(k0, k1, field, ctr, kPurposeOU << 24, up ? 2u : 1u, p);
+    float c0, s0, c1, s1;
+    box_muller(up ? p[0] : p[2], up ? p[1] : p[3], c0, s0);  // lower: slots 6,7   upper: 8,9
+    box_muller(p[2], p[3], c1, s1);                          // (lower: unused)    upper: 10,11
+    exch(c0, z[6], z[8]);
+    exch(s0, z[7], z[9]);
+    float unused;
+    exch(c1, unused, z[10]);
+    exch(s1, unused, z[11]);
+  }
+  constexpr int NL = MODE == VSS_MODE_SA ? 2 : 6;
+#pragma unroll
+  for (int k = NL; k < 12; ++k) a[k] = clampf((a[k] - K_OU_THETA * a[k]) + z[k], -1.0f, 1.0f);
+}
+
 // ---- the step kernel -------------------------------------------------------------------------------
 // One batch's inputs (kFpw fields of one wave), loaded into registers one batch ahead: the field's
 // bookkeeping and 46 live state channels, and the wave's contiguous AoS blocks of the batch's
@@ -994,6 +1046,8 @@ __global__ __launch_bounds__(kWave) VSS_STEP_ATTR void step_kernel(StepArgs args
 #pragma unroll
           for (int k = NL; k < 12; ++k) a[k] = clampf((a[k] - K_OU_THETA * a[k]) + z[k], -1.0f, 1.0f);
         }
+      } else if constexpr (kSplit) {
+        ou_noise_split<MODE>(a, k0, k1, (uint32_t)f, ctr);
       } else {
 #pragma unroll
         for (int blk = first_block; blk < 3; ++blk) {

@@ -46,6 +46,10 @@ def main():
     env = VSS(cfg, "cuda:0", "cuda:0", 0, True, False, False)
     mode_name = os.environ.get("ABLATE_MODE", "full")
     mode = {"full": N.MODE_FULL, "sa": N.MODE_SA, "cma": N.MODE_CMA, "dma": N.MODE_DMA}[mode_name]
+    # episodes desynchronised (progress uniform over the episode length): with every field at
+    # progress 0 the timeouts arrive in one burst every max_episode_length steps, and whether a
+    # burst of resets lands inside a variant's timed window decides its rollout figure
+    env.progress_buf.random_(0, int(cfg["env"]["maxEpisodeLength"]))
     prm, st = env._c_params(), env._c_state()
     if mode == N.MODE_FULL:
         acts = torch.rand((n, 12), device="cuda:0") * 2 - 1

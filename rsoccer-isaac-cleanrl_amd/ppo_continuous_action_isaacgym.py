@@ -233,9 +233,9 @@ class _TanhMLP(torch.autograd.Function):
 
 
 # the update's MLP path: "fused" (default) = _TanhMLP (our fp32 MFMA GEMMs with the tanh work in
-# their epilogues: 3.80 s per SA update at 65,536 envs); "split" = _LinearTanh / _LinearSplitK
-# (hipBLASLt GEMMs + the one-pass HIP tanh backward: 3.99 s).  DESIGN.md §5.3,
-# profiles/r01_gemm_fused_bench.log, profiles/r01_ppo_update_fused_vs_split.log.
+# their epilogues: 3.51 s per SA update at 65,536 envs); "split" = _LinearTanh / _LinearSplitK
+# (hipBLASLt GEMMs + the one-pass HIP tanh backward: 3.99 s).  DESIGN.md §5.3 / §7,
+# profiles/r02_gemm_fused_bench.log, profiles/r02_ppo_sa_fused_vs_split_seeds.json.
 UPDATE_MLP = os.environ.get("VSS_UPDATE_MLP", "fused")
 
 

@@ -66,3 +66,47 @@ def test_bench_two_ranks_rehearsal(launcher):
     ppo = j["ppo"]
     assert ppo["n_gpus"] == 2 and ppo["num_envs"] == 2 * 8192 and ppo["batch"] == 2 * 8192 * 128
     assert "all-reduce" in ppo["gradient_exchange"] and ppo["train_env_steps_per_s"] > 0
+
+
+_RCCL_SCRIPT = r"""
+import os, sys
+import torch, torch.distributed as dist
+sys.path.insert(0, {pkg!r})
+import ppo_continuous_action_isaacgym as P
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+assert dist.get_backend() == "nccl"
+dev = torch.device("cuda:0")
+net = torch.nn.Sequential(torch.nn.Linear(52, 256), torch.nn.Tanh(), torch.nn.Linear(256, 2)).to(dev)
+fg = P.FlatGrads(net)
+g = torch.Generator(device=dev).manual_seed(3)
+fg.flat.copy_(torch.randn(fg.flat.numel(), device=dev, generator=g))
+before = fg.flat.clone()
+dist.all_reduce(fg.flat, op=dist.ReduceOp.SUM)  # the DP gradient exchange's collective, one rank
+assert torch.equal(fg.flat, before)
+assert net[0].weight.grad.data_ptr() == fg.flat.data_ptr()
+adv = torch.randn(4096, device=dev, generator=g) * 3 + 1
+glob = P.normalize_advantages(adv, world=2, global_stats=True)  # the all-reduced (sum, sumsq, n) path
+loc = (adv - adv.mean()) / (adv.std() + 1e-8)
+assert torch.allclose(glob, loc, rtol=1e-5, atol=1e-5), (glob - loc).abs().max()
+t = torch.tensor([1.0, 2.0], dtype=torch.float64, device=dev)
+dist.all_reduce(t, op=dist.ReduceOp.MAX)  # bench.py's timing reduce
+assert t.tolist() == [1.0, 2.0]
+dist.barrier()
+dist.destroy_process_group()
+print("RCCL_OK")
+"""
+
+
+@pytest.mark.gpu
+def test_rccl_collectives_world1():
+    """The RCCL ("nccl") code path on the real GPU: process-group init with a device id (as
+    setup_distributed does for N>1), the flat-gradient all-reduce, the global advantage
+    statistics' all-reduce (normalize_advantages) and bench.py's max-reduce, one rank.  RCCL
+    refuses two ranks on one device, so more ranks than GPUs are rehearsed with gloo above."""
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    script = _RCCL_SCRIPT.format(pkg=os.path.join(REPO, "rsoccer-isaac-cleanrl_amd"))
+    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300, cwd=REPO,
+                       env=env)
+    assert r.returncode == 0 and "RCCL_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])

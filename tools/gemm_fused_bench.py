@@ -75,6 +75,7 @@ def main():
               flush=True)
         ref = torch.addmm(b, x, w.t()).tanh_()
         for name, lib in libs:
+            y.zero_()
             t_ours = timeit(lambda: lib.vss_linear_tanh(st, rows, k, n, x.data_ptr(), w.data_ptr(), b.data_ptr(),
                                                         y.data_ptr()))
             err = float((y - ref).abs().max())
@@ -97,6 +98,7 @@ def main():
         w_t = w_next.t().contiguous()
         for name, lib in libs:
             part = torch.empty(lib.vss_linear_tanh_backward_chunks(rows, kn, nn_), nn_, device="cuda")
+            out.zero_()
             t_ours = timeit(lambda: lib.vss_linear_tanh_backward(st, rows, kn, nn_, gz_next.data_ptr(), w_t.data_ptr(),
                                                                  yl.data_ptr(), out.data_ptr(), part.data_ptr()))
             err = float((out - ref).abs().max())

@@ -164,15 +164,6 @@ namespace vgemm {
 #ifndef VSS_LT_EXACT
 #define VSS_LT_EXACT 1  // unmasked loads for exact shapes
 #endif
-#ifndef VSS_LT_SPREAD
-#define VSS_LT_SPREAD 0  // 1: exact shapes with K % 64 == 0, K >= 192 run gemm_kernel_sp (spread epilogue, 128 x 128)
-#endif
-#ifndef VSS_LT_GL
-#define VSS_LT_GL 1  // 1: the spread-epilogue shapes run gemm_kernel_gl (LDS-DMA staging) instead of gemm_kernel_sp
-#endif
-#ifndef VSS_LT_NT
-#define VSS_LT_NT 0  // 1: gemm_kernel_gl streams its outputs and y with nontemporal stores / loads
-#endif
 #ifndef VSS_LT_NOMASK
 #define VSS_LT_NOMASK 1  // 1: gemm_kernel_d2 (exact shapes only) stores its epilogue without row masks
 #endif
@@ -624,430 +615,6 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel_d2(G
   }
 }
 
-// gemm_kernel_d2 with a SPREAD epilogue in the MFMA register layout (exact shapes, 128 x 128 blocks,
-// K = 64 NP).  Measured on gemm_kernel_d2 (profiles/r03_gemm_probe1.log): its K loop alone runs at
-// 0.87-0.91 of the fp32 MFMA peak, but the epilogue costs 12-22 % of the backward: its masked y loads
-// and stores compiled to `s_waitcnt vmcnt(0)` drains of the K tiles prefetched two ahead (vmcnt counts
-// loads and stores in one in-order counter), once per 32-row group.  Here:
-//  * the epilogue never goes through LDS: a lane keeps the 64 outputs of its MFMA tiles in `eo`
-//    (row (e & 3) + 8 (e >> 2) + 4 h, column lane & 31 of each 32 x 32 tile), every global access is
-//    one dword per lane, two full 128-B row segments per wave instruction;
-//  * the outputs are stored during the NEXT tile's K loop (after K-tile pairs 0 and 1), behind the
-//    loads already in flight, so no K-tile wait ever waits for a store;
-//  * the backward's y operand is loaded into the same registers after pairs 1 and 2, long before
-//    the epilogue reads it; the bias (a block always owns one column tile) is loaded once;
-//  * the K loop is straight-line code (NP is a template parameter) and the block's first tile is a
-//    separate instantiation, so the compiler's vmcnt counts stay exact (through a runtime loop, or
-//    at a join of paths with and without the stores, it waited for every outstanding load).
-// The MFMA sequence per output element is that of gemm_kernel_d2; the bias-gradient column sums are
-// summed in a different fixed order (per lane over its rows, then the two lane halves, then the row
-// waves): deterministic.
-template <int EPI, class C, int NP>
-__global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel_sp(GemmArgs p) {
-  constexpr int BM = C::BM, BN = C::BN, TM = C::TM, TN = C::TN, LROWS = C::LROWS, RA = C::RA, RB = C::RB;
-  static_assert(TM == 2 && TN == 2, "the spread epilogue's 4 store chunks are the wave's 4 MFMA tiles");
-  static_assert(NP >= 3, "the spread epilogue uses K-tile pairs 0-2");
-  constexpr int ktiles = 2 * NP;
-  __shared__ float lds[C::LDSF];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wv / C::WN, wn = wv % C::WN;
-  const int nb = p.n / BN;
-  const int K = p.k;
-  const int G = gridDim.x, tiles = (int)p.tiles;
-  const int slot = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  if (slot >= tiles) return;
-
-  const int lr = tid >> 3, lc = (tid & 7) * 4;
-  const int64_t KL = (int64_t)LROWS * K;
-  int f_tile = slot, f_kt = 0;
-  const float* fa;
-  const float* fb;
-  auto point = [&](int t) __attribute__((always_inline)) {
-    fa = p.a + ((int64_t)(t / nb) * BM + lr) * K + lc;
-    fb = p.b + ((int64_t)((t % nb) * BN) + lr) * K + lc;
-  };
-  point(f_tile);
-  auto advance = [&]() __attribute__((always_inline)) {
-    if (++f_kt < ktiles) {
-      fa += kKS;
-      fb += kKS;
-    } else if (f_tile + G < tiles) {
-      f_kt = 0;
-      f_tile += G;
-      point(f_tile);
-    } else {
-      f_kt = ktiles - 1;
-    }
-  };
-  auto gload = [&](float4 (&ra)[RA], float4 (&rb)[RB]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < RA; ++i) {
-      const vupd::f32x4 v = *reinterpret_cast<const vupd::f32x4*>(fa + i * KL);
-      ra[i] = make_float4(v.x, v.y, v.z, v.w);
-    }
-#pragma unroll
-    for (int i = 0; i < RB; ++i) {
-      const vupd::f32x4 v = *reinterpret_cast<const vupd::f32x4*>(fb + i * KL);
-      rb[i] = make_float4(v.x, v.y, v.z, v.w);
-    }
-    advance();
-  };
-  auto swrite = [&](const float4 (&ra)[RA], const float4 (&rb)[RB], int buf) __attribute__((always_inline)) {
-    float* As = lds + buf * (BM + BN) * kLS;
-    float* Bs = As + BM * kLS;
-#pragma unroll
-    for (int i = 0; i < RA; ++i) *reinterpret_cast<float4*>(As + (lr + LROWS * i) * kLS + lc) = ra[i];
-#pragma unroll
-    for (int i = 0; i < RB; ++i) *reinterpret_cast<float4*>(Bs + (lr + LROWS * i) * kLS + lc) = rb[i];
-  };
-  const int r = lane & 31, h = lane >> 5;
-  f32x16 acc[TM][TN];
-  auto mfma_tile = [&](int buf) __attribute__((always_inline)) {
-    const float* As = lds + buf * (BM + BN) * kLS + (wm * C::WROWS + r) * kLS + h * 16;
-    const float* Bs = lds + buf * (BM + BN) * kLS + BM * kLS + (wn * C::WCOLS + r) * kLS + h * 16;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float4 a4[TM], b4[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) a4[i] = *reinterpret_cast<const float4*>(As + i * 32 * kLS + q * 4);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) b4[j] = *reinterpret_cast<const float4*>(Bs + j * 32 * kLS + q * 4);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const float av = s == 0 ? a4[i].x : s == 1 ? a4[i].y : s == 2 ? a4[i].z : a4[i].w;
-            const float bv = s == 0 ? b4[j].x : s == 1 ? b4[j].y : s == 2 ? b4[j].z : b4[j].w;
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
-          }
-    }
-  };
-
-  // epilogue registers: eo[2 i + j][e] = element e of MFMA tile (i, j): row 32 i + (e & 3) + 8 (e >> 2)
-  // + 4 h, column 32 j + r of the wave's 64 x 64 block
-  const int64_t n64 = p.n;
-  float eo[TM * TN][16];
-  int64_t prev_off = 0;  // element offset of the previous tile's wave block, + this lane's (4 h, r)
-  auto store_chunk = [&](int c) __attribute__((always_inline)) {  // c = MFMA tile 2 i + j
-    const int i = c / 2, j = c % 2;
-#pragma unroll
-    for (int e = 0; e < 16; ++e)
-      p.out[prev_off + (int64_t)(32 * i + (e & 3) + 8 * (e >> 2)) * n64 + 32 * j] = eo[c][e];
-  };
-  auto yload_chunk = [&](int c, int64_t off) __attribute__((always_inline)) {
-    const int i = c / 2, j = c % 2;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) eo[c][e] = p.y[off + (int64_t)(32 * i + (e & 3) + 8 * (e >> 2)) * n64 + 32 * j];
-  };
-  float csum[TN] = {0.f, 0.f};  // EPI_DTANH: this lane's column sums (column 32 j + r) over its rows
-  // EPI_TANH: this lane's bias columns (G % nb == 0: a block always owns the same column tile), loaded
-  // once (a load in the epilogue would wait for every K-tile load issued before it)
-  float bcols[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) bcols[j] = EPI == EPI_TANH ? p.bias[(slot % nb) * BN + wn * C::WCOLS + j * 32 + r] : 0.0f;
-  float4 ra0[RA], rb0[RB], ra1[RA], rb1[RB];
-  auto kpair = [&]() __attribute__((always_inline)) {
-    mfma_tile(0);
-    swrite(ra1, rb1, 1);
-    __syncthreads();
-    gload(ra1, rb1);
-    mfma_tile(1);
-    swrite(ra0, rb0, 0);
-    __syncthreads();
-    gload(ra0, rb0);
-  };
-  // one output tile; STORE_PREV: eo holds the previous tile's outputs, stored during this K loop
-  auto run_tile = [&](auto store_prev, int tile) __attribute__((always_inline)) {
-    constexpr bool STORE_PREV = decltype(store_prev)::value;
-    const int64_t off = ((int64_t)(tile / nb) * BM + wm * C::WROWS + 4 * h) * n64 + (tile % nb) * BN + wn * C::WCOLS + r;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = (f32x16){0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    kpair();  // K tiles 0, 1
-    if constexpr (STORE_PREV) {
-      store_chunk(0);
-      store_chunk(1);
-    }
-    kpair();  // K tiles 2, 3
-    if constexpr (STORE_PREV) {
-      store_chunk(2);
-      store_chunk(3);
-    }
-    if constexpr (EPI == EPI_DTANH) {
-      yload_chunk(0, off);
-      yload_chunk(1, off);
-    }
-    kpair();  // K tiles 4, 5
-    if constexpr (EPI == EPI_DTANH) {
-      yload_chunk(2, off);
-      yload_chunk(3, off);
-    }
-#pragma unroll
-    for (int pp = 3; pp < NP; ++pp) kpair();
-    // epilogue, in registers
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const float v = acc[i][j][e];
-          if constexpr (EPI == EPI_TANH) {
-            eo[2 * i + j][e] = tanh_f32(v + bcols[j]);
-          } else {
-            const float yv = eo[2 * i + j][e];
-            const float g = v * fmaf(-yv, yv, 1.0f);
-            csum[j] += g;
-            eo[2 * i + j][e] = g;
-          }
-        }
-    prev_off = off;
-  };
-
-  gload(ra0, rb0);  // K tile 0
-  swrite(ra0, rb0, 0);
-  gload(ra1, rb1);  // K tile 1
-  gload(ra0, rb0);  // K tile 2
-  __syncthreads();
-  run_tile(std::false_type{}, slot);
-  for (int tile = slot + G; tile < tiles; tile += G) run_tile(std::true_type{}, tile);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) store_chunk(c);
-  if constexpr (EPI == EPI_DTANH) {
-    // column sums: the two lane halves (rows 4 h), then the WM row waves in order, into partial row
-    // slot / nb (the same layout as gemm_kernel_d2's)
-    __syncthreads();  // every wave is done with the LDS buffers
-#pragma unroll
-    for (int j = 0; j < TN; ++j) csum[j] += __shfl_xor(csum[j], 32);
-    if (h == 0) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) lds[wm * BN + wn * C::WCOLS + 32 * j + r] = csum[j];
-    }
-    __syncthreads();
-    if (tid < BN) {
-      float sacc = lds[tid];
-#pragma unroll
-      for (int m = 1; m < C::WM; ++m) sacc += lds[m * BN + tid];
-      p.partial[(int64_t)(slot / nb) * p.n + (slot % nb) * BN + tid] = sacc;
-    }
-  }
-}
-
-// gemm_kernel_gl: gemm_kernel_sp's epilogue with the operands staged by LDS DMA
-// (global_load_lds_dwordx4) instead of through registers: 64 VGPRs of staging freed, no ds_write
-// pass.  LDS image per buffer: the block's 128 A rows then 128 B rows of one K tile, 128 B each,
-// unpadded; float4 slot s of image row R holds k-group s ^ ((R >> 1) & 7) (a wave instruction
-// writes 1 KB = 8 rows contiguously, so the swizzle is applied to the per-lane SOURCE address);
-// the MFMA fragment reads (ds_read_b128, 16-lane groups over 16 consecutive rows at one k-group)
-// are conflict-free.  Two buffers, one K tile ahead: at K tile g every wave waits for its own DMA
-// of g (counted vmcnt), one barrier (all of g landed; every wave done reading g - 1's buffer), then
-// issues the DMA of g + 1 into the other buffer and multiplies g.
-namespace gl {
-constexpr uint32_t waitcnt_vm(int n) {  // s_waitcnt vmcnt(n), expcnt / lgkmcnt not waited (gfx9 encoding)
-  return (uint32_t)((n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8));
-}
-}  // namespace gl
-
-template <int EPI, int NP>
-__global__ __launch_bounds__(256, 2) void gemm_kernel_gl(GemmArgs p) {
-  constexpr int BM = 128, BN = 128, TM = 2, TN = 2, ktiles = 2 * NP;
-  constexpr int IMG = (BM + BN) * kKS;  // floats per LDS buffer
-  static_assert(NP >= 3, "the spread epilogue uses K-tile pairs 0-2");
-  // two separate LDS objects, so that the compiler's alias analysis sees that a DMA into one buffer
-  // does not write the other (with one array it waited for every DMA before each fragment read)
-  __shared__ __attribute__((aligned(1024))) float lds0[IMG];
-  __shared__ __attribute__((aligned(1024))) float lds1[IMG];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wv >> 1, wn = wv & 1;
-  const int nb = p.n / BN;
-  const int K = p.k;
-  const int G = gridDim.x, tiles = (int)p.tiles;
-  const int slot = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  if (slot >= tiles) return;
-
-  // DMA: wave wv stages image chunks 8 wv .. 8 wv + 7 (chunk c = image rows 8c .. 8c + 7): waves 0, 1
-  // the A rows, waves 2, 3 the B rows.  Lane l: row 8c + (l >> 3) of the chunk, slot l & 7, k-group
-  // (l & 7) ^ (4 (c & 1) + (l >> 4)); c & 1 = u & 1 for the wave's u-th chunk.
-  const float* const src = wv < 2 ? p.a : p.b;
-  const int src_row0 = (wv & 1) * 64;  // first image row of this wave's chunks, within A or B
-  uint32_t loff[2];
-#pragma unroll
-  for (int par = 0; par < 2; ++par)
-    loff[par] = (uint32_t)((src_row0 + (lane >> 3)) * K + (((lane & 7) ^ (4 * par + (lane >> 4))) * 4));
-  int f_tile = slot, f_kt = 0;  // the next K tile to stage
-  // The DMA is issued by inline asm: the compiler does not know that it writes LDS, so it neither
-  // waits for it before unrelated LDS reads (with the builtin it waited vmcnt(0) before every fragment
-  // read issued after a DMA: the DMA carries no alias information) nor moves it to the end of the K
-  // tile.  Its completion is ordered by the explicit `s_waitcnt vmcnt` + `s_barrier` before the
-  // buffer is read.
-  auto dma = [&](int buf) __attribute__((always_inline)) {
-    const int64_t rowbase = wv < 2 ? (int64_t)(f_tile / nb) * BM : (int64_t)(f_tile % nb) * BN;
-    const float* base = src + rowbase * K + f_kt * kKS;
-    float* dst = (buf ? lds1 : lds0) + wv * 8 * 256;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float* g = base + loff[u & 1] + u * 8 * K;
-      const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)(dst + u * 256);
-      asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(la) : "memory");
-    }
-    // cursor: the next K tile; past the block's last tile it re-stages that tile's last K tile (never read)
-    const bool wrap = ++f_kt == ktiles, more = f_tile + G < tiles;
-    f_tile = wrap && more ? f_tile + G : f_tile;
-    f_kt = wrap ? (more ? 0 : ktiles - 1) : f_kt;
-  };
-  const int r = lane & 31, h = lane >> 5;
-  const int sw = (r >> 1) & 7;
-  f32x16 acc[TM][TN];
-  auto mfma_tile = [&](int buf) __attribute__((always_inline)) {
-    const float* As = (buf ? lds1 : lds0) + (wm * 64 + r) * kKS;
-    const float* Bs = (buf ? lds1 : lds0) + (BM + wn * 64 + r) * kKS;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int sl = ((4 * h + q) ^ sw) * 4;
-      float4 a4[TM], b4[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) a4[i] = *reinterpret_cast<const float4*>(As + i * 32 * kKS + sl);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) b4[j] = *reinterpret_cast<const float4*>(Bs + j * 32 * kKS + sl);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const float av = s == 0 ? a4[i].x : s == 1 ? a4[i].y : s == 2 ? a4[i].z : a4[i].w;
-            const float bv = s == 0 ? b4[j].x : s == 1 ? b4[j].y : s == 2 ? b4[j].z : b4[j].w;
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
-          }
-    }
-  };
-
-  // The epilogue is deferred into the next tile's K loop, one MFMA tile (chunk) of the wave per K
-  // tile, so that its VALU work and memory ops are issued among the MFMAs instead of in a phase where
-  // the SIMD's matrix pipe idles.  Forward: at a tile's end the accumulators are only copied to `eo`;
-  // in K tile c of the next tile chunk c gets its bias + tanh and its stores.  Backward: y chunk c is
-  // loaded into eo in K tile c + 1 (after the previous tile's chunk c was stored from there in K tile
-  // c), the tile's end computes eo = acc (1 - y^2) and the column sums, the stores follow in the next
-  // tile's K tiles 0-3.
-  const int64_t n64 = p.n;
-  float eo[TM * TN][16];  // MFMA layout: element e of chunk 2 i + j = row 32 i + (e & 3) + 8 (e >> 2) + 4 h, column 32 j + r
-  // addresses: a wave-uniform element offset (a tile's wave block) + this lane's 32-bit offset (row
-  // 4 h, column r), so that no 64-bit address per element stays live
-  int64_t prev_off = 0;
-  const uint32_t lane_off = (uint32_t)(4 * h * p.n + r);
-  auto row_off = [&](int64_t base, int c, int e) __attribute__((always_inline)) {
-    return base + (int64_t)(32 * (c / 2) + (e & 3) + 8 * (e >> 2)) * n64 + 32 * (c % 2);
-  };
-  float csum[TN] = {0.f, 0.f};
-  float bcols[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) bcols[j] = EPI == EPI_TANH ? p.bias[(slot % nb) * BN + wn * 64 + j * 32 + r] : 0.0f;
-  auto finish = [&](int c) __attribute__((always_inline)) {  // the previous tile's chunk c: (tanh,) store
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const float o = EPI == EPI_TANH ? tanh_f32(eo[c][e] + bcols[c % 2]) : eo[c][e];
-#if VSS_LT_PROBE == 5 || VSS_LT_PROBE == 6
-      asm volatile("" ::"v"(o));
-#else
-      (p.out + row_off(prev_off, c, e))[lane_off] = o;
-#endif
-    }
-  };
-  auto yload = [&](int64_t off, int c) __attribute__((always_inline)) {
-#pragma unroll
-    for (int e = 0; e < 16; ++e) eo[c][e] = (p.y + row_off(off, c, e))[lane_off];
-  };
-  auto vm_issued = [&](int kt, bool sp) -> int {  // vm ops the deferred work of K tile kt issues
-#if VSS_LT_PROBE == 5 || VSS_LT_PROBE == 6
-    const int st = 0;
-#else
-    const int st = sp && kt < 4 ? 16 : 0;
-#endif
-#if VSS_LT_PROBE == 6
-    return 0;
-#else
-    return st + (EPI == EPI_DTANH && kt >= 1 && kt <= 4 ? 16 : 0);
-#endif
-  };
-  // before the barrier: this wave's DMA of the buffer about to be read has landed (vmcnt), and its
-  // fragment reads of the buffer the next DMA overwrites have returned (lgkmcnt); asm, so that the
-  // compiler keeps it as written
-  auto wait_vm = [&](int n) __attribute__((always_inline)) {
-    if (n == 0)
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else if (n == 16)
-      asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)" ::: "memory");
-  };
-  auto run_tile = [&](auto store_prev, int tile) __attribute__((always_inline)) {
-    constexpr bool SP = decltype(store_prev)::value;
-    const int64_t off = ((int64_t)(tile / nb) * BM + wm * 64) * n64 + (tile % nb) * BN + wn * 64;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = (f32x16){0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kt = 0; kt < ktiles; ++kt) {
-      // this wave's DMA of K tile kt has landed (the vm ops issued after it: the previous K tile's
-      // deferred work), then every wave's; buffer (kt + 1) & 1 is free
-      wait_vm(kt == 0 ? 0 : vm_issued(kt - 1, SP));
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");  // LDS contents change here (the other waves' DMAs)
-      dma((kt + 1) & 1);
-      mfma_tile(kt & 1);
-      if constexpr (SP) {
-        if (kt < 4) finish(kt);
-      }
-#if VSS_LT_PROBE != 6
-      if constexpr (EPI == EPI_DTANH) {
-        if (kt >= 1 && kt <= 4) yload(off, kt - 1);
-      }
-#endif
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          if constexpr (EPI == EPI_TANH) {
-            eo[2 * i + j][e] = acc[i][j][e];
-          } else {
-            const float yv = eo[2 * i + j][e];
-            const float g = acc[i][j][e] * fmaf(-yv, yv, 1.0f);
-            csum[j] += g;
-            eo[2 * i + j][e] = g;
-          }
-        }
-    prev_off = off;
-  };
-
-  dma(0);  // K tile 0 of the first tile
-  run_tile(std::false_type{}, slot);
-  for (int tile = slot + G; tile < tiles; tile += G) run_tile(std::true_type{}, tile);
-  // the last tile's epilogue
-#pragma unroll
-  for (int c = 0; c < 4; ++c) finish(c);
-  if constexpr (EPI == EPI_DTANH) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < TN; ++j) csum[j] += __shfl_xor(csum[j], 32);
-    if (h == 0) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) lds0[wm * BN + wn * 64 + 32 * j + r] = csum[j];
-    }
-    __syncthreads();
-    if (tid < BN) p.partial[(int64_t)(slot / nb) * p.n + (slot % nb) * BN + tid] = lds0[tid] + lds0[BN + tid];
-  }
-}
-
 // The persistent grid is sized for MI355X (256 CUs) on every device: a block walks its tiles however
 // many blocks are resident, so the grid -- and with it the bias-gradient partial layout and its
 // summation order -- does not depend on the device the call runs on.
@@ -1077,7 +644,6 @@ static Plan plan(int64_t rows, int32_t k, int32_t n, bool forward) {
   if (VSS_LT_D2CFG == 256 && VSS_LT_DEPTH == 2 && forward && exact && rows % Cfg256::BM == 0 && k % (2 * kKS) == 0 &&
       n % 256 == 0)
     pl.kind = 1;
-  if (VSS_LT_SPREAD && exact && (k == 256 || k == 512)) pl.kind = 0;  // gemm_kernel_sp
   static const int BMs[2] = {Cfg128::BM, Cfg256::BM};
   static const int BNs[2] = {Cfg128::BN, Cfg256::BN};
   static const int BPC[2] = {Cfg128::BLOCKS_PER_CU, Cfg256::BLOCKS_PER_CU};
@@ -1105,20 +671,6 @@ static bool shape_ok(int64_t rows, int32_t k, int32_t n) {
 template <int EPI, bool EXACT>
 static void launch_kind(const GemmArgs& a, const Plan& pl, hipStream_t s) {
   const dim3 grid((unsigned)pl.grid);
-  if (VSS_LT_SPREAD && VSS_LT_GL && EXACT && pl.kind == 0 && (a.k == 256 || a.k == 512)) {
-    if (a.k == 256)
-      hipLaunchKernelGGL((gemm_kernel_gl<EPI, 4>), grid, dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((gemm_kernel_gl<EPI, 8>), grid, dim3(256), 0, s, a);
-    return;
-  }
-  if (VSS_LT_SPREAD && EXACT && pl.kind == 0 && (a.k == 256 || a.k == 512)) {
-    if (a.k == 256)
-      hipLaunchKernelGGL((gemm_kernel_sp<EPI, Cfg128, 4>), grid, dim3(Cfg128::THREADS), 0, s, a);
-    else
-      hipLaunchKernelGGL((gemm_kernel_sp<EPI, Cfg128, 8>), grid, dim3(Cfg128::THREADS), 0, s, a);
-    return;
-  }
   if (VSS_LT_DEPTH == 2 && EXACT && pl.kind == 0 && a.k % (2 * kKS) == 0) {
     hipLaunchKernelGGL((gemm_kernel_d2<EPI, Cfg128>), grid, dim3(Cfg128::THREADS), 0, s, a);
     return;

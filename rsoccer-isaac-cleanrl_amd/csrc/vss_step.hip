@@ -15,6 +15,7 @@
 // Everything is float32 with FMA contraction disabled (-ffp-contract=off and the pragma
 // below): results are bit-identical to the CPU oracle (oracle/vss_oracle.c).
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 
 #include "../../include/vss.h"
@@ -163,8 +164,10 @@ __device__ __forceinline__ void philox(uint32_t k0, uint32_t k1, uint32_t c0, ui
                                        uint32_t c3, uint32_t out[4]) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-    uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-    uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    // one 32 x 32 -> 64-bit product each (v_mad_u64_u32) instead of separate mul_hi / mul_lo
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
     uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
@@ -521,27 +524,65 @@ __device__ __forceinline__ void physics_split(Bodies& b, const float a[12]) {
 __device__ __forceinline__ void wait_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 // ---- state I/O -----------------------------------------------------------------------------------
-__device__ __forceinline__ void load_bodies(const float* __restrict__ st, int64_t n, int64_t f, Bodies& b) {
-  b.bx = st[VSS_CH_BALL_X * n + f]; b.by = st[VSS_CH_BALL_Y * n + f];
-  b.bvx = st[VSS_CH_BALL_VX * n + f]; b.bvy = st[VSS_CH_BALL_VY * n + f];
+// Addressing: a wave's accesses are a wave-uniform base (field f0 of a channel: ch * n + f0, in SGPRs)
+// plus the lane's 32-bit byte offset, so they compile to `global_load/store v, v_off, s[base]`.
+// Written as one int64 index (ch * n + f0 + fl) the compiler formed every address per lane with two
+// quarter-rate v_mad_u64_u32 (the multiply by n fused into the divergent add): 46 channel loads and
+// 46 stores, ~400 VALU slots per wave.  uni() launders the base through readfirstlane so it is not
+// re-associated with the lane offset.
+#ifndef VSS_UNI
+#define VSS_UNI 0  // profiling knob: 1 = bases laundered through readfirstlane (measured ~1 us slower per step)
+#endif
+#ifndef VSS_BODY_WALK
+#define VSS_BODY_WALK 1  // profiling knob: 0 = state channels addressed as st[ch * n + f]
+#endif
+template <class T>
+__device__ __forceinline__ T* uni(T* p) {
+  if (!VSS_UNI) return p;
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
+// element at (wave-uniform base) + byte offset
+template <class T>
+__device__ __forceinline__ T& at(T* base, uint32_t byte_off) {
+  using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+  return *reinterpret_cast<T*>(reinterpret_cast<B*>(uni(base)) + byte_off);
+}
+
+// fields f0 + fl (f0 wave-uniform).  The channels are walked with one running per-lane pointer
+// advanced by the channel stride (n floats, wave-uniform): one 64-bit add per channel.
+__device__ __forceinline__ void load_bodies(const float* __restrict__ st, int64_t n, int64_t f0, int fl, Bodies& b) {
+  float v[VSS_STATE_CHANNELS];
+  const float* q = st + f0 + fl;
+#pragma unroll
+  for (int c = 0; c < VSS_STATE_CHANNELS; ++c) {
+    if (c < VSS_CH_RQX || c >= VSS_CH_RQZ)  // the quaternions' x, y channels are not live (planar)
+      v[c] = VSS_BODY_WALK ? *q : st[c * n + f0 + fl];
+    q += n;
+  }
+  b.bx = v[VSS_CH_BALL_X]; b.by = v[VSS_CH_BALL_Y]; b.bvx = v[VSS_CH_BALL_VX]; b.bvy = v[VSS_CH_BALL_VY];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    b.x[i] = st[(VSS_CH_RX + i) * n + f]; b.y[i] = st[(VSS_CH_RY + i) * n + f];
-    b.qz[i] = st[(VSS_CH_RQZ + i) * n + f]; b.qw[i] = st[(VSS_CH_RQW + i) * n + f];
-    b.vx[i] = st[(VSS_CH_RVX + i) * n + f]; b.vy[i] = st[(VSS_CH_RVY + i) * n + f];
-    b.w[i] = st[(VSS_CH_RW + i) * n + f];
+    b.x[i] = v[VSS_CH_RX + i]; b.y[i] = v[VSS_CH_RY + i]; b.qz[i] = v[VSS_CH_RQZ + i]; b.qw[i] = v[VSS_CH_RQW + i];
+    b.vx[i] = v[VSS_CH_RVX + i]; b.vy[i] = v[VSS_CH_RVY + i]; b.w[i] = v[VSS_CH_RW + i];
   }
 }
 
-__device__ __forceinline__ void store_bodies(float* __restrict__ st, int64_t n, int64_t f, const Bodies& b) {
-  st[VSS_CH_BALL_X * n + f] = b.bx; st[VSS_CH_BALL_Y * n + f] = b.by;
-  st[VSS_CH_BALL_VX * n + f] = b.bvx; st[VSS_CH_BALL_VY * n + f] = b.bvy;
+__device__ __forceinline__ void store_bodies(float* __restrict__ st, int64_t n, int64_t f0, int fl, const Bodies& b) {
+  float v[VSS_STATE_CHANNELS];
+  v[VSS_CH_BALL_X] = b.bx; v[VSS_CH_BALL_Y] = b.by; v[VSS_CH_BALL_VX] = b.bvx; v[VSS_CH_BALL_VY] = b.bvy;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    st[(VSS_CH_RX + i) * n + f] = b.x[i]; st[(VSS_CH_RY + i) * n + f] = b.y[i];
-    st[(VSS_CH_RQZ + i) * n + f] = b.qz[i]; st[(VSS_CH_RQW + i) * n + f] = b.qw[i];
-    st[(VSS_CH_RVX + i) * n + f] = b.vx[i]; st[(VSS_CH_RVY + i) * n + f] = b.vy[i];
-    st[(VSS_CH_RW + i) * n + f] = b.w[i];
+    v[VSS_CH_RX + i] = b.x[i]; v[VSS_CH_RY + i] = b.y[i]; v[VSS_CH_RQZ + i] = b.qz[i]; v[VSS_CH_RQW + i] = b.qw[i];
+    v[VSS_CH_RVX + i] = b.vx[i]; v[VSS_CH_RVY + i] = b.vy[i]; v[VSS_CH_RW + i] = b.w[i];
+  }
+  float* q = st + f0 + fl;
+#pragma unroll
+  for (int c = 0; c < VSS_STATE_CHANNELS; ++c) {
+    if (c < VSS_CH_RQX || c >= VSS_CH_RQZ) (VSS_BODY_WALK ? *q : st[c * n + f0 + fl]) = v[c];
+    q += n;
   }
 }
 
@@ -553,7 +594,7 @@ __device__ __forceinline__ void coop_load(const float* __restrict__ g, int nv, f
   if constexpr (W % 4 == 0) {
     const float4* g4 = reinterpret_cast<const float4*>(g);
     for (int q = lane; q < total / 4; q += kWave) {
-      float4 v = g4[q];
+      float4 v = at(g4, 16u * (uint32_t)q);
       int e = q * 4, fl = e / W, k = e - fl * W;
       float* d = lds + fl * kRec + k;
       d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
@@ -561,7 +602,7 @@ __device__ __forceinline__ void coop_load(const float* __restrict__ g, int nv, f
   } else {
     const float2* g2 = reinterpret_cast<const float2*>(g);
     for (int q = lane; q < total / 2; q += kWave) {
-      float2 v = g2[q];
+      float2 v = at(g2, 8u * (uint32_t)q);
       int e = q * 2, fl = e / W, k = e - fl * W;
       float* d = lds + fl * kRec + k;
       d[0] = v.x; d[1] = v.y;
@@ -577,14 +618,14 @@ __device__ __forceinline__ void coop_store(float* __restrict__ g, int nv, const 
     for (int q = lane; q < total / 4; q += kWave) {
       int e = q * 4, fl = e / W, k = e - fl * W;
       const float* s = lds + fl * kRec + k;
-      g4[q] = make_float4(s[0], s[1], s[2], s[3]);
+      at(g4, 16u * (uint32_t)q) = make_float4(s[0], s[1], s[2], s[3]);
     }
   } else {
     float2* g2 = reinterpret_cast<float2*>(g);
     for (int q = lane; q < total / 2; q += kWave) {
       int e = q * 2, fl = e / W, k = e - fl * W;
       const float* s = lds + fl * kRec + k;
-      g2[q] = make_float2(s[0], s[1]);
+      at(g2, 8u * (uint32_t)q) = make_float2(s[0], s[1]);
     }
   }
 }
@@ -648,7 +689,7 @@ __device__ __forceinline__ void coop_store_obs(float* __restrict__ out, int nv, 
     }
 #pragma unroll
     for (int u = 0; u < kObsUnroll; ++u)
-      if (q0 + u * kWave < total) o4[q0 + u * kWave] = v[u];
+      if (q0 + u * kWave < total) at(o4, 16u * (uint32_t)(q0 + u * kWave)) = v[u];
   }
 }
 
@@ -836,7 +877,7 @@ __device__ __forceinline__ void prefetch12(const float* __restrict__ g, int nv, 
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int q = lane + j * kWave;
-    if (q < nv * 3) pre[j] = g4[q];
+    if (q < nv * 3) pre[j] = at(g4, 16u * (uint32_t)q);
   }
 }
 
@@ -860,7 +901,7 @@ __device__ __forceinline__ void prefetch_lrn(const float* __restrict__ g, int nv
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int q = lane + j * kWave;
-    if (q < nv * NL / 2) pre[j] = g2[q];
+    if (q < nv * NL / 2) pre[j] = at(g2, 8u * (uint32_t)q);
   }
 }
 
@@ -956,16 +997,15 @@ struct StepArgs {
 template <int MODE>
 __device__ __forceinline__ void load_batch(const StepArgs& args, int64_t f0, int nv, int fl, int lane, BatchIn& in) {
   constexpr int NL = MODE == VSS_MODE_SA ? 2 : 6;
-  const int64_t f = f0 + fl;
   in.progress = 0;
   in.reset_prev = 0;
   in.ctr = 0;
   in.b = {};
   if (fl < nv) {
-    in.progress = args.s.progress_buf[f];
-    in.reset_prev = args.s.reset_buf[f];
-    in.ctr = args.s.rng_counter[f];
-    load_bodies(args.s.state, args.n, f, in.b);
+    in.progress = at(args.s.progress_buf + f0, 8u * (uint32_t)fl);
+    in.reset_prev = at(args.s.reset_buf + f0, 8u * (uint32_t)fl);
+    in.ctr = at(args.s.rng_counter + f0, 4u * (uint32_t)fl);
+    load_bodies(args.s.state, args.n, f0, fl, in.b);
   }
   prefetch12((MODE == VSS_MODE_FULL ? args.io.actions : args.io.ou_buf) + f0 * 12, nv, lane, in.blk);
   if constexpr (MODE != VSS_MODE_FULL) prefetch_lrn<NL>(args.io.actions + f0 * NL, nv, lane, in.lrn);
@@ -1142,18 +1182,19 @@ __global__ __launch_bounds__(kWave) VSS_STEP_ATTR void step_kernel(StepArgs args
     // -- bookkeeping --------------------------------------------------------------------------------------------
     const uint8_t time_out = (progress >= (int64_t)args.p.max_episode_length - 1) && done != 0;
     if (owner) {
-      store_bodies(args.s.state, n, f, b);
-      args.s.progress_buf[f] = progress;
-      args.s.reset_buf[f] = done;
-      args.s.rng_counter[f] = ctr + 1u;
+      const uint32_t ufl = (uint32_t)fl;
+      store_bodies(args.s.state, n, f0, fl, b);
+      at(args.s.progress_buf + f0, 8u * ufl) = progress;
+      at(args.s.reset_buf + f0, 8u * ufl) = done;
+      at(args.s.rng_counter + f0, 4u * ufl) = ctr + 1u;
 #pragma unroll
       for (int k = 0; k < R; ++k) {
-        args.io.time_outs[f * R + k] = time_out;
-        args.io.progress_f[f * R + k] = (float)progress;
+        at(args.io.time_outs + f0 * R, (uint32_t)(ufl * R + k)) = time_out;
+        at(args.io.progress_f + f0 * R, 4u * (ufl * R + k)) = (float)progress;
       }
       if constexpr (MODE == VSS_MODE_DMA) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) args.io.dones_rep[f * 3 + k] = done;
+        for (int k = 0; k < 3; ++k) at(args.io.dones_rep + f0 * 3, 8u * (ufl * 3 + k)) = done;
       }
     }
 
@@ -1183,19 +1224,19 @@ __global__ __launch_bounds__(kWave) VSS_STEP_ATTR void step_kernel(StepArgs args
       }
       __syncthreads();
       coop_store<24>(args.io.rew + f0 * 24, nv, lds, lane);
-      if (owner && args.io.reward_sum) args.io.reward_sum[f] = ((rew[0] + rew[1]) + rew[2]) + rew[3];
+      if (owner && args.io.reward_sum) at(args.io.reward_sum + f0, 4u * (uint32_t)fl) = ((rew[0] + rew[1]) + rew[2]) + rew[3];
     } else if constexpr (MODE == VSS_MODE_SA) {
       if (owner) {
-        reinterpret_cast<float4*>(args.io.rew)[f] = make_float4(rew[0], rew[1], rew[2], rew[3]);
-        args.io.reward_sum[f] = ((rew[0] + rew[1]) + rew[2]) + rew[3];
+        at(reinterpret_cast<float4*>(args.io.rew) + f0, 16u * (uint32_t)fl) = make_float4(rew[0], rew[1], rew[2], rew[3]);
+        at(args.io.reward_sum + f0, 4u * (uint32_t)fl) = ((rew[0] + rew[1]) + rew[2]) + rew[3];
       }
     } else if constexpr (MODE == VSS_MODE_CMA) {
       if (owner) {
         float m[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) m[c] = ((rew[c] + rew[4 + c]) + rew[8 + c]) / 3.0f;
-        reinterpret_cast<float4*>(args.io.rew)[f] = make_float4(m[0], m[1], m[2], m[3]);
-        args.io.reward_sum[f] = ((m[0] + m[1]) + m[2]) + m[3];
+        at(reinterpret_cast<float4*>(args.io.rew) + f0, 16u * (uint32_t)fl) = make_float4(m[0], m[1], m[2], m[3]);
+        at(args.io.reward_sum + f0, 4u * (uint32_t)fl) = ((m[0] + m[1]) + m[2]) + m[3];
       }
     } else {
       if (writer) {
@@ -1207,7 +1248,8 @@ __global__ __launch_bounds__(kWave) VSS_STEP_ATTR void step_kernel(StepArgs args
       if (owner) {
 #pragma unroll
         for (int ag = 0; ag < 3; ++ag)
-          args.io.reward_sum[f * 3 + ag] = ((rew[4 * ag] + rew[4 * ag + 1]) + rew[4 * ag + 2]) + rew[4 * ag + 3];
+          at(args.io.reward_sum + f0 * 3, 4u * ((uint32_t)fl * 3 + ag)) =
+              ((rew[4 * ag] + rew[4 * ag + 1]) + rew[4 * ag + 2]) + rew[4 * ag + 3];
       }
     }
     if (!more) break;
@@ -1253,10 +1295,10 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
   uint32_t ctr = 0;
   Bodies b = {};
   if (valid) {
-    progress = args.s.progress_buf[f];
-    reset_prev = args.s.reset_buf[f];
-    ctr = args.s.rng_counter[f];
-    load_bodies(args.s.state, n, f, b);
+    progress = at(args.s.progress_buf + f0, 8u * (uint32_t)fl);
+    reset_prev = at(args.s.reset_buf + f0, 8u * (uint32_t)fl);
+    ctr = at(args.s.rng_counter + f0, 4u * (uint32_t)fl);
+    load_bodies(args.s.state, n, f0, fl, b);
   }
   float4 pre[3];
   prefetch12(args.io.actions + f0 * 12, nv, lane, pre);
@@ -1323,7 +1365,7 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
   }
 
   if (owner) {
-    store_bodies(args.s.state, n, f, b);
+    store_bodies(args.s.state, n, f0, fl, b);
     args.s.progress_buf[f] = progress;
     args.s.reset_buf[f] = done;
     args.s.rng_counter[f] = ctr + (uint32_t)args.k_steps;
@@ -1345,12 +1387,13 @@ __global__ __launch_bounds__(kWave) void reset_kernel(int64_t n, vss_params p, v
   const int64_t f = (int64_t)blockIdx.x * kWave + threadIdx.x;
   if (f >= n || s.reset_buf[f] == 0) return;
   Bodies b;
-  load_bodies(s.state, n, f, b);
+  const int64_t f0 = (int64_t)blockIdx.x * kWave;
+  load_bodies(s.state, n, f0, (int)threadIdx.x, b);
   const uint32_t ctr = s.rng_counter[f];
   const ResetDraws rd{(uint32_t)p.seed, (uint32_t)(p.seed >> 32), (uint32_t)f, ctr, kExternal,
                       REPLAY ? rdr.uniforms + f * rdr.uniform_stride : nullptr, REPLAY ? rounds : (uint32_t)kMaxRejectRounds};
   reset_field<REPLAY>(b, rd);
-  store_bodies(s.state, n, f, b);
+  store_bodies(s.state, n, f0, (int)threadIdx.x, b);
   s.rng_counter[f] = ctr + 1u;
 #pragma unroll
   for (int k = 0; k < 12; ++k) s.dof_velocity_buf[f * 12 + k] = s.dof_velocity_buf[f * 12 + k] * 0.0f;
@@ -1364,7 +1407,7 @@ __global__ __launch_bounds__(kWave) void observe_kernel(int64_t n, vss_state s, 
   const int lane = threadIdx.x;
   const int64_t f0 = (int64_t)blockIdx.x * kWave;
   const int nv = (int)(n - f0 < kWave ? n - f0 : kWave);
-  const int64_t f = f0 + lane;
+
   float* rec = lds + lane * kRec;
   float* orec = lds + lane * obs_rec<A>();
   coop_load<12>(s.dof_velocity_buf + f0 * 12, nv, lds, lane);
@@ -1375,7 +1418,7 @@ __global__ __launch_bounds__(kWave) void observe_kernel(int64_t n, vss_state s, 
   __syncthreads();
   Bodies b = {};
   if (lane < nv) {
-    load_bodies(s.state, n, f, b);
+    load_bodies(s.state, n, f0, lane, b);
     write_obs_record<A>(orec, b, dof);
   }
   wait_loads();

@@ -600,9 +600,10 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel_d2(G
 #pragma unroll
         for (int e = 0; e < 16; ++e) asm volatile("" ::"v"(acc[i][j][e]));
 #else
-    // exact shapes: no row masks (their branches made the compiler drain vmcnt to 0, i.e. wait for the
-    // K tiles prefetched two ahead, at every y load and store)
-    store_tile<EPI, TM, TN, !VSS_LT_NOMASK>(p, acc, lds + (BM + BN) * kLS + wv * (32 * kES), row0 + wm * C::WROWS,
+    // backward, exact shapes: no row masks (their branches made the compiler drain vmcnt to 0, i.e.
+    // wait for the K tiles prefetched two ahead, at every y load; the forward measured ~1 % slower
+    // without them, profiles/r02_gemm_epilogue_variants.log)
+    store_tile<EPI, TM, TN, !(VSS_LT_NOMASK && EPI == EPI_DTANH)>(p, acc, lds + (BM + BN) * kLS + wv * (32 * kES), row0 + wm * C::WROWS,
                                             col0 + wn * C::WCOLS, csum);
 #endif
     if (!has_next) break;

@@ -1034,6 +1034,14 @@ __global__ __launch_bounds__(kWave) VSS_STEP_ATTR void step_kernel(StepArgs args
   if (blockIdx.x & 1)
     for (int i = 0; i < VSS_PROF_STAGGER; ++i) __builtin_amdgcn_s_sleep(64);
 #endif
+#ifdef VSS_PRIO_HALF  // profiling knob: the first half of the grid (each SIMD's first wave) runs at raised priority
+  if (blockIdx.x < gridDim.x / 2) __builtin_amdgcn_s_setprio(VSS_PRIO_HALF);
+#endif
+#ifdef VSS_PROF_STAGGER_HALF  // profiling knob: the second half of the grid (dispatched as each SIMD's
+  // second wave) starts VSS_PROF_STAGGER_HALF x 16 x 64 cycles late
+  if (blockIdx.x >= gridDim.x / 2)
+    for (int i = 0; i < VSS_PROF_STAGGER_HALF; ++i) __builtin_amdgcn_s_sleep(16);
+#endif
 
   const int64_t n = args.n;
   const int lane = threadIdx.x;
@@ -1137,6 +1145,9 @@ __global__ __launch_bounds__(kWave) VSS_STEP_ATTR void step_kernel(StepArgs args
     }
 #endif
 
+#if defined(VSS_PRIO_HALF) && defined(VSS_PRIO_PHYS_ONLY)
+    __builtin_amdgcn_s_setprio(0);
+#endif
     // -- post_physics_step: progress, rewards, dones (envs/vss.py:189-265) ----------------------------------
     progress += 1;
     float rew[24];

@@ -660,8 +660,13 @@ __device__ __forceinline__ void write_obs_record(float* rec, const Bodies& b, co
 // incrementally; four LDS reads per float4 at table-given byte offsets, one 16-B store.  Unrolled
 // by kObsUnroll so the LDS latency of U slots overlaps (reads past the last field are clamped to
 // the last record and their stores predicated off).
+//
+// NT: nontemporal stores.  Measured (profiles/r02_ablate_nt_obs.log): the wrapped modes' steps are
+// 2-5 % faster with them (SA 21.2 -> 20.5 us, CMA 21.5 -> 20.4, DMA 28.1 -> 27.6); the FULL step,
+// whose 164 MB of observation streams fit the 256 MiB Infinity Cache at 65,536 fields, is 11 % slower
+// (38.3 -> 42.5 us; 1.6 % faster past the cache at 131,072 fields), so FULL keeps plain stores.
 constexpr int kObsUnroll = 4;
-template <int A>
+template <int A, bool NT = false>
 __device__ __forceinline__ void coop_store_obs(float* __restrict__ out, int nv, const float* lds, const uint32_t* tab,
                                                int lane) {
   constexpr int Q = 13 * A;  // float4 per field
@@ -689,7 +694,15 @@ __device__ __forceinline__ void coop_store_obs(float* __restrict__ out, int nv, 
     }
 #pragma unroll
     for (int u = 0; u < kObsUnroll; ++u)
-      if (q0 + u * kWave < total) at(o4, 16u * (uint32_t)(q0 + u * kWave)) = v[u];
+      if (q0 + u * kWave < total) {
+        if constexpr (NT) {
+          typedef float f4v __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(f4v{v[u].x, v[u].y, v[u].z, v[u].w},
+                                      reinterpret_cast<f4v*>(&at(o4, 16u * (uint32_t)(q0 + u * kWave))));
+        } else {
+          at(o4, 16u * (uint32_t)(q0 + u * kWave)) = v[u];
+        }
+      }
   }
 }
 
@@ -1163,7 +1176,7 @@ __global__ __launch_bounds__(kWave) VSS_STEP_ATTR void step_kernel(StepArgs args
     if (lane < kFpw) write_obs_record<A>(orec, b, a);
     __syncthreads();
 #ifndef VSS_PROF_SKIP_OBS
-    coop_store_obs<A>(args.io.terminal_obs + f0 * (52 * A), nv, lds, tab, lane);
+    coop_store_obs<A, MODE != VSS_MODE_FULL>(args.io.terminal_obs + f0 * (52 * A), nv, lds, tab, lane);
 #endif
     __syncthreads();
 
@@ -1186,7 +1199,7 @@ __global__ __launch_bounds__(kWave) VSS_STEP_ATTR void step_kernel(StepArgs args
     if (lane < kFpw) write_obs_record<A>(orec, b, dof);
     __syncthreads();
 #ifndef VSS_PROF_SKIP_OBS
-    coop_store_obs<A>(args.io.obs + f0 * (52 * A), nv, lds, tab, lane);
+    coop_store_obs<A, MODE != VSS_MODE_FULL>(args.io.obs + f0 * (52 * A), nv, lds, tab, lane);
 #endif
     __syncthreads();
 

@@ -661,14 +661,19 @@ __device__ __forceinline__ void write_obs_record(float* rec, const Bodies& b, co
 // by kObsUnroll so the LDS latency of U slots overlaps (reads past the last field are clamped to
 // the last record and their stores predicated off).
 //
-// NT: nontemporal stores.  Measured (profiles/r02_ablate_nt_obs.log): the wrapped modes' steps are
-// 2-5 % faster with them (SA 21.2 -> 20.5 us, CMA 21.5 -> 20.4, DMA 28.1 -> 27.6); the FULL step,
-// whose 164 MB of observation streams fit the 256 MiB Infinity Cache at 65,536 fields, is 11 % slower
-// (38.3 -> 42.5 us; 1.6 % faster past the cache at 131,072 fields), so FULL keeps plain stores.
+// nt: nontemporal stores (profiles/r02_ablate_nt_obs.log).  The wrapped modes' steps are 2-5 %
+// faster with both observation streams nontemporal (SA 21.3 -> 20.5 us, CMA 21.5 -> 20.4, DMA
+// 28.4 -> 27.7).  The FULL step streams 164 MB of observations per 65,536 fields: while its whole
+// footprint fits the 256 MiB Infinity Cache plain stores are best (both streams nontemporal: 11 %
+// slower, one: +0.5 %); past it, one stream nontemporal and the other plain is best (131,072
+// fields: 74.5 -> 68.4 us; both nontemporal: +1.6 % only), so the host sets StepArgs::nt_obs for
+// footprints above the cache size and FULL then streams `obs` nontemporally, `terminal_obs` plain.
+// The K-step rollout (K x 175 MB per launch) streams both nontemporally: 36.1 -> 33.3 us per step at
+// K = 16 (obs alone: no gain).
 constexpr int kObsUnroll = 4;
-template <int A, bool NT = false>
+template <int A>
 __device__ __forceinline__ void coop_store_obs(float* __restrict__ out, int nv, const float* lds, const uint32_t* tab,
-                                               int lane) {
+                                               int lane, bool nt = false) {
   constexpr int Q = 13 * A;  // float4 per field
   constexpr int QD = kWave / Q, QR = kWave % Q;
   constexpr uint32_t RB = 4u * obs_rec<A>();  // record bytes
@@ -695,7 +700,7 @@ __device__ __forceinline__ void coop_store_obs(float* __restrict__ out, int nv, 
 #pragma unroll
     for (int u = 0; u < kObsUnroll; ++u)
       if (q0 + u * kWave < total) {
-        if constexpr (NT) {
+        if (nt) {  // wave-uniform
           typedef float f4v __attribute__((ext_vector_type(4)));
           __builtin_nontemporal_store(f4v{v[u].x, v[u].y, v[u].z, v[u].w},
                                       reinterpret_cast<f4v*>(&at(o4, 16u * (uint32_t)(q0 + u * kWave))));
@@ -1002,6 +1007,7 @@ struct StepArgs {
   vss_step_io io;
   vss_replay_draws rd;  // REPLAY instantiations only (vss_step_replay)
   uint32_t rd_rounds;   // rejection rounds one replay row holds
+  uint32_t nt_obs;      // FULL: stream obs with nontemporal stores (footprint past the Infinity Cache)
 };
 
 // REPLAY = false: the product kernel (Philox draws).  REPLAY = true: the parity entry
@@ -1176,7 +1182,7 @@ __global__ __launch_bounds__(kWave) VSS_STEP_ATTR void step_kernel(StepArgs args
     if (lane < kFpw) write_obs_record<A>(orec, b, a);
     __syncthreads();
 #ifndef VSS_PROF_SKIP_OBS
-    coop_store_obs<A, MODE != VSS_MODE_FULL>(args.io.terminal_obs + f0 * (52 * A), nv, lds, tab, lane);
+    coop_store_obs<A>(args.io.terminal_obs + f0 * (52 * A), nv, lds, tab, lane, MODE != VSS_MODE_FULL);
 #endif
     __syncthreads();
 
@@ -1199,7 +1205,7 @@ __global__ __launch_bounds__(kWave) VSS_STEP_ATTR void step_kernel(StepArgs args
     if (lane < kFpw) write_obs_record<A>(orec, b, dof);
     __syncthreads();
 #ifndef VSS_PROF_SKIP_OBS
-    coop_store_obs<A, MODE != VSS_MODE_FULL>(args.io.obs + f0 * (52 * A), nv, lds, tab, lane);
+    coop_store_obs<A>(args.io.obs + f0 * (52 * A), nv, lds, tab, lane, MODE != VSS_MODE_FULL || args.nt_obs != 0);
 #endif
     __syncthreads();
 
@@ -1358,7 +1364,7 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
     wait_loads();
     if (lane < kFpwRollout) write_obs_record<6>(orec, b, a);
     __syncthreads();
-    coop_store_obs<6>(args.io.terminal_obs + (step_off + f0) * 312, nv, lds, tab, lane);
+    coop_store_obs<6>(args.io.terminal_obs + (step_off + f0) * 312, nv, lds, tab, lane, true);  // K steps: past the cache
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 12; ++i) dof[i] = a[i];
@@ -1371,7 +1377,7 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
     }
     if (lane < kFpwRollout) write_obs_record<6>(orec, b, dof);
     __syncthreads();
-    coop_store_obs<6>(args.io.obs + (step_off + f0) * 312, nv, lds, tab, lane);
+    coop_store_obs<6>(args.io.obs + (step_off + f0) * 312, nv, lds, tab, lane, true);
     __syncthreads();
     if (writer) {
 #pragma unroll
@@ -1513,7 +1519,10 @@ static int step_impl(void* stream, int64_t n, int32_t mode, const vss_params* p,
     if (rounds < 1 || (mode != VSS_MODE_FULL && bad(rd->normals, 4))) return VSS_E_ARG;
   }
   if (n == 0) return VSS_OK;
-  vss::StepArgs args{n, *p, *st, *io, REPLAY ? *rd : vss_replay_draws{}, (uint32_t)rounds};
+  // FULL: the observation stream nontemporal once the step's footprint (3,101 B per field) is past
+  // the 256 MiB Infinity Cache (coop_store_obs)
+  const uint32_t nt_obs = mode == VSS_MODE_FULL && n > (int64_t)(256ll << 20) / 3101 ? 1u : 0u;
+  vss::StepArgs args{n, *p, *st, *io, REPLAY ? *rd : vss_replay_draws{}, (uint32_t)rounds, nt_obs};
   const int fpw = mode == VSS_MODE_FULL ? vss::fields_per_wave<VSS_MODE_FULL>()
                   : mode == VSS_MODE_SA ? vss::fields_per_wave<VSS_MODE_SA>()
                   : mode == VSS_MODE_CMA ? vss::fields_per_wave<VSS_MODE_CMA>() : vss::fields_per_wave<VSS_MODE_DMA>();

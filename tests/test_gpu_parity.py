@@ -99,6 +99,31 @@ def test_full_step_free_running_bit_exact(n, steps, max_len):
     assert resets > 0 and goals > 0 and timeouts > 0
 
 
+def test_full_step_past_infinity_cache_bit_exact():
+    """98,304 fields: the FULL footprint (3,101 B per field) is past the 256 MiB Infinity Cache, so
+    the host sets nt_obs and the kernel streams `obs` with nontemporal stores (vss_step.hip,
+    coop_store_obs).  Same bar as the free-running tests: every output bit-exact vs the oracle,
+    over steps that include time-outs and resets."""
+    n, steps = 98304, 3
+    assert n > (256 << 20) // 3101
+    env = make_vss(n, max_len=2)
+    h = host_from(env)
+    prm = oracle_params(env)
+    gen = np.random.default_rng(7)
+    for t in range(steps):
+        a = gen.uniform(-1.0, 1.0, (n, 2, 3, 2)).astype(np.float32)
+        obs_dict, rew, reset, extras = env.step(torch.from_numpy(a).to(DEV))
+        io = O.make_io(n, O.MODE_FULL)
+        O.step(h, O.MODE_FULL, a.reshape(n, 12), io, prm)
+        msg = f"step {t}"
+        assert_env_equal(env, h, msg)
+        np.testing.assert_array_equal(bits(obs_dict["obs"]).reshape(n, 312), io["obs"].view(np.uint32).reshape(n, 312), err_msg=msg)
+        np.testing.assert_array_equal(bits(extras["terminal_observation"]).reshape(n, 312),
+                                      io["terminal_obs"].view(np.uint32).reshape(n, 312), err_msg=msg)
+        np.testing.assert_array_equal(bits(rew).reshape(n, 24), io["rew"].view(np.uint32), err_msg=msg)
+    assert int(h.reset.sum()) > 0
+
+
 @pytest.mark.parametrize("weights,clip", [((1.0, 0.0, 0.0, 0.0), 1.0),     # play.py's evaluation weights
                                           ((10.0, 2.0, 3.0, 0.5), 1.0),    # energy term on
                                           ((0.0, 0.0, 0.0, 0.0), 0.5),     # every term off, tighter clip

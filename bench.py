@@ -208,8 +208,8 @@ def rollout_leg(env, K: int, steps: int, gen, dev) -> dict:
     the state / bookkeeping / dof read+write (456 B) once per launch."""
     n = env.num_fields
     # episodes desynchronised (progress uniform over the episode length, as in a running training
-    # loop): after the FULL leg every field sits at the same progress, and whether the resulting
-    # burst of time-out resets fell inside the 12 timed launches decided this figure (29.8 vs 33.6 us)
+    # loop) rather than all at the progress the FULL leg left; the progress distribution was measured
+    # not to move this figure (profiles/r02_rollout_progress_distribution.log)
     env.progress_buf.random_(0, int(env.max_episode_length), generator=gen)
     acts = torch.rand((K, n, 2, 3, 2), device=dev, generator=gen) * 2 - 1
     out = env.rollout(acts)

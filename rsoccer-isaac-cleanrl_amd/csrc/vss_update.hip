@@ -201,15 +201,20 @@ struct Cfg {
   static constexpr int WROWS = BM / WM, WCOLS = BN / WN;
   static constexpr int TM = WROWS / 32, TN = WCOLS / 32;
   static constexpr int LDSF = 2 * (BM + BN) * kLS;  // two K-tile buffers
+  // gemm_kernel_d2's epilogue scratch starts at K-tile buffer 1 and may run past it (8 waves of
+  // 64 x 64 on 128 x 256 blocks): the kernel's LDS is then sized to cover it
+  static constexpr int SCR = WM * WN * 32 * kES;
+  static constexpr int LDSA = LDSF + (SCR > (BM + BN) * kLS ? SCR - (BM + BN) * kLS : 0);
   static constexpr int LROWS = THREADS / 8;          // rows one staging pass covers (8 float4 per 32-float row)
   static constexpr int RA = BM / LROWS, RB = BN / LROWS;
-  static constexpr int BLOCKS_PER_CU = LDSF * 4 * 2 <= 160 * 1024 ? 2 : 1;
+  static constexpr int BLOCKS_PER_CU = LDSA * 4 * 2 <= 160 * 1024 ? 2 : 1;
   static_assert(WCOLS == 64, "the epilogue streams 64-column wave tiles");
-  static_assert(WM * WN * 32 * kES <= (BM + BN) * kLS, "epilogue scratch must fit one K-tile buffer");
   static_assert(RA * LROWS == BM && RB * LROWS == BN, "staging passes must tile the block");
 };
-using Cfg128 = Cfg<128, 128, 2, 2>;  // 4 waves, 72 KB LDS: two blocks per CU
-using Cfg256 = Cfg<256, 256, 2, 4>;  // 8 waves of 128 x 64, 144 KB LDS: one block per CU
+using Cfg128 = Cfg<128, 128, 2, 2>;     // 4 waves, 72 KB LDS: two blocks per CU
+using Cfg256 = Cfg<256, 256, 2, 4>;     // 8 waves of 128 x 64, 144 KB LDS: one block per CU
+using Cfg128x256 = Cfg<128, 256, 2, 4>; // 8 waves of 64 x 64, 126 KB LDS: one block per CU
+using Cfg256x128 = Cfg<256, 128, 4, 2>; // 8 waves of 64 x 64, 126 KB LDS: one block per CU
 
 struct GemmArgs {
   int64_t rows;
@@ -319,6 +324,7 @@ __device__ __forceinline__ void write_colsums(const GemmArgs& p, float4 csum, fl
 template <int EPI, class C, bool EXACT>
 __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(GemmArgs p) {
   constexpr int BM = C::BM, BN = C::BN, TM = C::TM, TN = C::TN, LROWS = C::LROWS;
+  static_assert(C::SCR <= (BM + BN) * kLS, "epilogue scratch must fit one K-tile buffer");
   __shared__ float lds[C::LDSF];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv / C::WN, wn = wv % C::WN;
   const int nb = p.n / BN;
@@ -479,7 +485,7 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(Gemm
 template <int EPI, class C>
 __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel_d2(GemmArgs p) {
   constexpr int BM = C::BM, BN = C::BN, TM = C::TM, TN = C::TN, LROWS = C::LROWS, RA = C::RA, RB = C::RB;
-  __shared__ float lds[C::LDSF];
+  __shared__ float lds[C::LDSA];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv / C::WN, wn = wv % C::WN;
   const int nb = p.n / BN;
   const int K = p.k, ktiles = K / kKS;  // even (K % 64 == 0)
@@ -634,9 +640,13 @@ constexpr int kGridCus = 256;
 #define VSS_LT_CFG 256  // 256: 256 x 256 blocks for masked shapes with n % 256 == 0; 128: always 128 x 128
 #endif
 
+#ifndef VSS_LT_BWDCFG
+#define VSS_LT_BWDCFG 0  // backward exact shapes: 0 = 128 x 128 blocks, 2 = 128 x 256, 3 = 256 x 128
+#endif
+
 // the launch plan of one GEMM: kernel, output tiles, grid
 struct Plan {
-  int kind;  // 0 Cfg128, 1 Cfg256
+  int kind;  // 0 Cfg128, 1 Cfg256, 2 Cfg128x256, 3 Cfg256x128
   int bn;
   int64_t tiles, grid;
 };
@@ -654,9 +664,16 @@ static Plan plan(int64_t rows, int32_t k, int32_t n, bool forward) {
   if (VSS_LT_D2CFG == 256 && VSS_LT_DEPTH == 2 && forward && exact && rows % Cfg256::BM == 0 && k % (2 * kKS) == 0 &&
       n % 256 == 0)
     pl.kind = 1;
-  static const int BMs[2] = {Cfg128::BM, Cfg256::BM};
-  static const int BNs[2] = {Cfg128::BN, Cfg256::BN};
-  static const int BPC[2] = {Cfg128::BLOCKS_PER_CU, Cfg256::BLOCKS_PER_CU};
+  if (VSS_LT_BWDCFG == 2 && VSS_LT_DEPTH == 2 && !forward && exact && rows % Cfg128x256::BM == 0 && k % (2 * kKS) == 0 &&
+      n % Cfg128x256::BN == 0)
+    pl.kind = 2;
+  if (VSS_LT_BWDCFG == 3 && VSS_LT_DEPTH == 2 && !forward && exact && rows % Cfg256x128::BM == 0 && k % (2 * kKS) == 0 &&
+      n % Cfg256x128::BN == 0)
+    pl.kind = 3;
+  static const int BMs[4] = {Cfg128::BM, Cfg256::BM, Cfg128x256::BM, Cfg256x128::BM};
+  static const int BNs[4] = {Cfg128::BN, Cfg256::BN, Cfg128x256::BN, Cfg256x128::BN};
+  static const int BPC[4] = {Cfg128::BLOCKS_PER_CU, Cfg256::BLOCKS_PER_CU, Cfg128x256::BLOCKS_PER_CU,
+                             Cfg256x128::BLOCKS_PER_CU};
   const int bm = BMs[pl.kind];
   pl.bn = BNs[pl.kind];
   const int nb = n / pl.bn;
@@ -681,6 +698,16 @@ static bool shape_ok(int64_t rows, int32_t k, int32_t n) {
 template <int EPI, bool EXACT>
 static void launch_kind(const GemmArgs& a, const Plan& pl, hipStream_t s) {
   const dim3 grid((unsigned)pl.grid);
+  if constexpr (EPI == EPI_DTANH && EXACT) {
+    if (pl.kind == 2) {
+      hipLaunchKernelGGL((gemm_kernel_d2<EPI_DTANH, Cfg128x256>), grid, dim3(Cfg128x256::THREADS), 0, s, a);
+      return;
+    }
+    if (pl.kind == 3) {
+      hipLaunchKernelGGL((gemm_kernel_d2<EPI_DTANH, Cfg256x128>), grid, dim3(Cfg256x128::THREADS), 0, s, a);
+      return;
+    }
+  }
   if (VSS_LT_DEPTH == 2 && EXACT && pl.kind == 0 && a.k % (2 * kKS) == 0) {
     hipLaunchKernelGGL((gemm_kernel_d2<EPI, Cfg128>), grid, dim3(Cfg128::THREADS), 0, s, a);
     return;
@@ -699,7 +726,8 @@ template <int EPI>
 static int launch(void* stream, const GemmArgs& a0, const Plan& pl) {
   GemmArgs a = a0;
   a.tiles = pl.tiles;
-  const int bm = pl.kind == 1 ? Cfg256::BM : Cfg128::BM;
+  static const int BMs[4] = {Cfg128::BM, Cfg256::BM, Cfg128x256::BM, Cfg256x128::BM};
+  const int bm = BMs[pl.kind];
   const bool exact = VSS_LT_EXACT && a.rows % bm == 0 && a.k % kKS == 0;
   if (exact)
     launch_kind<EPI, true>(a, pl, (hipStream_t)stream);

@@ -94,7 +94,7 @@ def main():
         fl = 2.0 * rows * kn * nn_
         print(f"BWD K {kn:3d} N {nn_:3d}: torch mm + tanh_grad_bias {t_ref:7.0f} us (mm {t_gemm:7.0f} us = "
               f"{fl / t_gemm / 1e6:5.1f} TF)", flush=True)
-        ref, _ = tanh_grad_bias(gz_next.mm(w_next), yl)
+        ref, ref_bias = tanh_grad_bias(gz_next.mm(w_next), yl)
         w_t = w_next.t().contiguous()
         for name, lib in libs:
             part = torch.empty(lib.vss_linear_tanh_backward_chunks(rows, kn, nn_), nn_, device="cuda")
@@ -102,7 +102,9 @@ def main():
             t_ours = timeit(lambda: lib.vss_linear_tanh_backward(st, rows, kn, nn_, gz_next.data_ptr(), w_t.data_ptr(),
                                                                  yl.data_ptr(), out.data_ptr(), part.data_ptr()))
             err = float((out - ref).abs().max())
-            print(f"    {name:12s} {t_ours:7.0f} us = {fl / t_ours / 1e6:5.1f} TF   max|diff| {err:.2e}", flush=True)
+            berr = float((part.sum(0) - ref_bias).abs().max() / ref_bias.abs().max())
+            print(f"    {name:12s} {t_ours:7.0f} us = {fl / t_ours / 1e6:5.1f} TF   max|diff| {err:.2e}   bias rel {berr:.1e}",
+                  flush=True)
         del gz_next, yl, out, ref
 
 

@@ -736,6 +736,95 @@ static int launch(void* stream, const GemmArgs& a0, const Plan& pl) {
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 
+// ---- the output layer's backward: k_next = 4 or 8 (the 1, 2 or 6 output columns, zero-padded) ------
+// gz = (gz_next W_next) * (1 - y^2) with a contraction of 4 or 8 is a streaming pass over y and gz
+// (2 x 4 B per element, ~2 k FLOP per element), not a GEMM: on the masked MFMA path it padded K to
+// a 32-wide K tile and ran the MFMAs, then the epilogue, one after the other (1.02 ms at 2,097,152 x
+// 256, 4.1 TB/s).  Here every thread owns 4 columns with their k_next weights in registers, a block
+// walks a contiguous band of rows with four rows in flight per thread, gz streams out
+// nontemporally, and the block's column sums land in partial[block] (one fixed summation order).
+constexpr int kSmallThreads = 256;
+constexpr int kSmallMaxBlocks = 2048;
+
+struct SmallPlan {
+  int64_t rows_per_block, blocks;
+};
+
+#ifndef VSS_LT_SMALLK
+#define VSS_LT_SMALLK 1  // profiling knob: 0 = the output layer's backward on the masked MFMA path
+#endif
+
+static bool small_k(int32_t k_next, int32_t n) {
+  return VSS_LT_SMALLK && (k_next == 4 || k_next == 8) && 1024 % n == 0;
+}
+
+static SmallPlan small_plan(int64_t rows, int32_t n) {
+  const int64_t rpp = kSmallThreads / (n / 4);  // rows one pass of the block covers
+  int64_t g = (rows + rpp - 1) / rpp;
+  if (g > kSmallMaxBlocks) g = kSmallMaxBlocks;
+  int64_t per = (rows + g - 1) / g;
+  per = (per + rpp - 1) / rpp * rpp;
+  return SmallPlan{per, (rows + per - 1) / per};
+}
+
+template <int KN>
+__global__ __launch_bounds__(kSmallThreads) void dtanh_small_k_kernel(int64_t rows, int n, const float* __restrict__ g,
+                                                                      const float* __restrict__ wt,
+                                                                      const float* __restrict__ y, float* __restrict__ out,
+                                                                      float* __restrict__ partial, int64_t per) {
+  __shared__ float4 red[kSmallThreads];
+  const int tpr = n >> 2, rpp = kSmallThreads / tpr;
+  const int tid = threadIdx.x, c = (tid % tpr) * 4, ro = tid / tpr;
+  float w[4][KN];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int a = 0; a < KN; ++a) w[j][a] = wt[(int64_t)(c + j) * KN + a];
+  float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int64_t r0 = (int64_t)blockIdx.x * per;
+  const int64_t r1 = r0 + per < rows ? r0 + per : rows;
+  constexpr int U = 4;
+  for (int64_t rb = r0 + ro; rb < r1; rb += (int64_t)U * rpp) {
+    float4 yv[U], gv[U][KN / 4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = rb + (int64_t)u * rpp;
+      if (row < r1) {
+        yv[u] = *reinterpret_cast<const float4*>(y + row * n + c);
+#pragma unroll
+        for (int q = 0; q < KN / 4; ++q) gv[u][q] = *reinterpret_cast<const float4*>(g + row * KN + 4 * q);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = rb + (int64_t)u * rpp;
+      if (row < r1) {
+        const float* gr = reinterpret_cast<const float*>(gv[u]);
+        float acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float t = gr[0] * w[j][0];
+#pragma unroll
+          for (int a = 1; a < KN; ++a) t = fmaf(gr[a], w[j][a], t);
+          acc[j] = t;
+        }
+        const float4 yq = yv[u];
+        const vupd::f32x4 v = {acc[0] * fmaf(-yq.x, yq.x, 1.0f), acc[1] * fmaf(-yq.y, yq.y, 1.0f),
+                               acc[2] * fmaf(-yq.z, yq.z, 1.0f), acc[3] * fmaf(-yq.w, yq.w, 1.0f)};
+        __builtin_nontemporal_store(v, reinterpret_cast<vupd::f32x4*>(out + row * n + c));
+        cs.x += v[0]; cs.y += v[1]; cs.z += v[2]; cs.w += v[3];
+      }
+    }
+  }
+  red[tid] = cs;
+  __syncthreads();
+  if (tid < tpr) {
+    float4 s4 = red[tid];
+    for (int m = 1; m < rpp; ++m) vupd::add4(s4, red[m * tpr + tid]);
+    *reinterpret_cast<float4*>(partial + (int64_t)blockIdx.x * n + c) = s4;
+  }
+}
+
 }  // namespace vgemm
 
 extern "C" {
@@ -785,6 +874,7 @@ int vss_linear_tanh(void* stream, int64_t rows, int32_t k_in, int32_t n_out, con
 int64_t vss_linear_tanh_backward_chunks(int64_t rows, int32_t k_next, int32_t n_out) {
   if (!vgemm::shape_ok(rows, k_next, n_out)) return -1;
   if (rows == 0) return 0;
+  if (vgemm::small_k(k_next, n_out)) return vgemm::small_plan(rows, n_out).blocks;
   const vgemm::Plan pl = vgemm::plan(rows, k_next, n_out, false);
   return pl.grid / (n_out / pl.bn);
 }
@@ -795,6 +885,17 @@ int vss_linear_tanh_backward(void* stream, int64_t rows, int32_t k_next, int32_t
       misaligned(grad_in) || misaligned(bias_partial))
     return VSS_E_ARG;
   if (rows == 0) return VSS_OK;
+  if (vgemm::small_k(k_next, n_out)) {
+    const vgemm::SmallPlan sp = vgemm::small_plan(rows, n_out);
+    const dim3 grid((unsigned)sp.blocks), block(vgemm::kSmallThreads);
+    if (k_next == 4)
+      hipLaunchKernelGGL(vgemm::dtanh_small_k_kernel<4>, grid, block, 0, (hipStream_t)stream, rows, n_out, grad_next,
+                         w_next_t, y, grad_in, bias_partial, sp.rows_per_block);
+    else
+      hipLaunchKernelGGL(vgemm::dtanh_small_k_kernel<8>, grid, block, 0, (hipStream_t)stream, rows, n_out, grad_next,
+                         w_next_t, y, grad_in, bias_partial, sp.rows_per_block);
+    return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+  }
   const vgemm::GemmArgs a{rows, n_out, k_next, grad_next, w_next_t, nullptr, y, grad_in, bias_partial, 0};
   return vgemm::launch<vgemm::EPI_DTANH>(stream, a, vgemm::plan(rows, k_next, n_out, false));
 }

@@ -127,7 +127,8 @@ def test_linear_tanh_small_arguments_keep_relative_precision_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k_next,n", [(256, 512), (512, 512), (512, 256), (4, 128), (64, 256)])
+@pytest.mark.parametrize("k_next,n", [(256, 512), (512, 512), (512, 256), (4, 128), (64, 256), (4, 256), (8, 512),
+                                      (8, 384)])
 @pytest.mark.parametrize("rows", [1, 127, 129, 4133, 70_000, 65_536])
 def test_linear_tanh_backward_gpu(rows, k_next, n):
     """vss_linear_tanh_backward vs fp64: gz = (gz_next @ w_next) * (1 - y^2) and db = gz.sum(0);

@@ -284,6 +284,22 @@ int64_t vss_linear_tanh_backward_chunks(int64_t rows, int32_t k_next, int32_t n_
 int vss_linear_tanh_backward(void* stream, int64_t rows, int32_t k_next, int32_t n_out, const float* grad_next,
                              const float* w_next_t, const float* y, float* grad_in, float* bias_partial);
 
+/* The Agent's output layer backward in one streaming pass (ppo_continuous_action_isaacgym.py:104-111
+ * under loss.backward(), :357): for the output nn.Linear (k_out = 1, 2 or 6 columns, g_out and its
+ * weight zero-padded by the caller to k_pad = 4 or 8 columns / rows) over a tanh layer of width n
+ * (n in {128, 256, 512, 1024}):
+ *   grad_in = (g_out W_out) * (1 - y^2)        the tanh layer's pre-activation gradient (rows, n)
+ *   bias_partial (chunks, n)                   column-sum parts of grad_in (its bias gradient)
+ *   wgrad_partial (chunks, k_pad, n)           parts of g_out^T y, the output layer's weight gradient
+ * g_out (rows, k_pad), w_out_t (n, k_pad) = the padded weight TRANSPOSED, y (rows, n) = the tanh
+ * output (the output layer's input); chunks = vss_output_backward_chunks(rows, k_pad, n) (-1 for a
+ * bad shape), summed in a fixed order by the caller.  Every pointer 16-B aligned.  Replaces the
+ * output layer's dX GEMM + tanh_backward + bias reduction and its dW GEMM (two reads of y -> one).
+ */
+int64_t vss_output_backward_chunks(int64_t rows, int32_t k_pad, int32_t n);
+int vss_output_backward(void* stream, int64_t rows, int32_t k_pad, int32_t n, const float* g_out, const float* w_out_t,
+                        const float* y, float* grad_in, float* bias_partial, float* wgrad_partial);
+
 /* ---------------------------------------------------------------------------------------------
  * Episode statistics: RecordEpisodeStatisticsTorch.step (envs/wrappers.py:66-87)
  * for `rows` learner rows in one launch, in the reference's order:

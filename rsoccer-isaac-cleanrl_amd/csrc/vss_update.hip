@@ -767,12 +767,18 @@ static SmallPlan small_plan(int64_t rows, int32_t n) {
   return SmallPlan{per, (rows + per - 1) / per};
 }
 
-template <int KN>
+// WG (vss_output_backward): the same pass also accumulates the output layer's weight gradient
+// g_out^T y (its input is y) from the values it already holds, as per-block partials (KN x n).
+template <int KN, bool WG = false>
 __global__ __launch_bounds__(kSmallThreads) void dtanh_small_k_kernel(int64_t rows, int n, const float* __restrict__ g,
                                                                       const float* __restrict__ wt,
                                                                       const float* __restrict__ y, float* __restrict__ out,
-                                                                      float* __restrict__ partial, int64_t per) {
+                                                                      float* __restrict__ partial, int64_t per,
+                                                                      float* __restrict__ wpartial = nullptr) {
   __shared__ float4 red[kSmallThreads];
+  float4 wacc[WG ? KN : 1];
+#pragma unroll
+  for (int a = 0; a < (WG ? KN : 1); ++a) wacc[a] = make_float4(0.f, 0.f, 0.f, 0.f);
   const int tpr = n >> 2, rpp = kSmallThreads / tpr;
   const int tid = threadIdx.x, c = (tid % tpr) * 4, ro = tid / tpr;
   float w[4][KN];
@@ -813,6 +819,13 @@ __global__ __launch_bounds__(kSmallThreads) void dtanh_small_k_kernel(int64_t ro
                                acc[2] * fmaf(-yq.z, yq.z, 1.0f), acc[3] * fmaf(-yq.w, yq.w, 1.0f)};
         __builtin_nontemporal_store(v, reinterpret_cast<vupd::f32x4*>(out + row * n + c));
         cs.x += v[0]; cs.y += v[1]; cs.z += v[2]; cs.w += v[3];
+        if constexpr (WG) {
+#pragma unroll
+          for (int a = 0; a < KN; ++a) {
+            wacc[a].x = fmaf(gr[a], yq.x, wacc[a].x); wacc[a].y = fmaf(gr[a], yq.y, wacc[a].y);
+            wacc[a].z = fmaf(gr[a], yq.z, wacc[a].z); wacc[a].w = fmaf(gr[a], yq.w, wacc[a].w);
+          }
+        }
       }
     }
   }
@@ -822,6 +835,19 @@ __global__ __launch_bounds__(kSmallThreads) void dtanh_small_k_kernel(int64_t ro
     float4 s4 = red[tid];
     for (int m = 1; m < rpp; ++m) vupd::add4(s4, red[m * tpr + tid]);
     *reinterpret_cast<float4*>(partial + (int64_t)blockIdx.x * n + c) = s4;
+  }
+  if constexpr (WG) {
+#pragma unroll
+    for (int a = 0; a < KN; ++a) {
+      __syncthreads();
+      red[tid] = wacc[a];
+      __syncthreads();
+      if (tid < tpr) {
+        float4 s4 = red[tid];
+        for (int m = 1; m < rpp; ++m) vupd::add4(s4, red[m * tpr + tid]);
+        *reinterpret_cast<float4*>(wpartial + ((int64_t)blockIdx.x * KN + a) * n + c) = s4;
+      }
+    }
   }
 }
 
@@ -898,6 +924,29 @@ int vss_linear_tanh_backward(void* stream, int64_t rows, int32_t k_next, int32_t
   }
   const vgemm::GemmArgs a{rows, n_out, k_next, grad_next, w_next_t, nullptr, y, grad_in, bias_partial, 0};
   return vgemm::launch<vgemm::EPI_DTANH>(stream, a, vgemm::plan(rows, k_next, n_out, false));
+}
+
+int64_t vss_output_backward_chunks(int64_t rows, int32_t k_pad, int32_t n) {
+  if (rows < 0 || rows > (int64_t(1) << 40) || (k_pad != 4 && k_pad != 8) || n < 128 || n % 128 != 0 || 1024 % n != 0)
+    return -1;
+  return rows == 0 ? 0 : vgemm::small_plan(rows, n).blocks;
+}
+
+int vss_output_backward(void* stream, int64_t rows, int32_t k_pad, int32_t n, const float* g_out, const float* w_out_t,
+                        const float* y, float* grad_in, float* bias_partial, float* wgrad_partial) {
+  if (vss_output_backward_chunks(rows, k_pad, n) < 0 || misaligned(g_out) || misaligned(w_out_t) || misaligned(y) ||
+      misaligned(grad_in) || misaligned(bias_partial) || misaligned(wgrad_partial))
+    return VSS_E_ARG;
+  if (rows == 0) return VSS_OK;
+  const vgemm::SmallPlan sp = vgemm::small_plan(rows, n);
+  const dim3 grid((unsigned)sp.blocks), block(vgemm::kSmallThreads);
+  if (k_pad == 4)
+    hipLaunchKernelGGL((vgemm::dtanh_small_k_kernel<4, true>), grid, block, 0, (hipStream_t)stream, rows, n, g_out,
+                       w_out_t, y, grad_in, bias_partial, sp.rows_per_block, wgrad_partial);
+  else
+    hipLaunchKernelGGL((vgemm::dtanh_small_k_kernel<8, true>), grid, block, 0, (hipStream_t)stream, rows, n, g_out,
+                       w_out_t, y, grad_in, bias_partial, sp.rows_per_block, wgrad_partial);
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 
 }  // extern "C"

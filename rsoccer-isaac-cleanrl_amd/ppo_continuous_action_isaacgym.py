@@ -34,7 +34,8 @@ from torch.distributions.normal import Normal
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from envs._gym import Box, ObservationWrapper  # noqa: E402
-from vss_amd.update import gemm_shape_ok, linear_tanh, linear_tanh_backward, tanh_grad_bias  # noqa: E402
+from vss_amd.update import (gemm_shape_ok, linear_tanh, linear_tanh_backward, output_backward,  # noqa: E402
+                            output_backward_ok, tanh_grad_bias)
 
 
 def strtobool(x: str) -> bool:
@@ -218,6 +219,12 @@ class _TanhMLP(torch.autograd.Function):
         gz = gout.contiguous()  # pre-activation gradient of the current layer
         gb = gz.sum(0)
         for layer in reversed(range(n)):
+            if OUTPUT_BWD and layer == n - 1 and layer > 0 and output_backward_ok(gz.shape[1], hs[layer].shape[1]):
+                # the output layer (1-6 columns): its weight gradient and the backward into the tanh
+                # layer below in one streaming pass over that layer's output (vss_output_backward)
+                grads[2 * layer + 1] = gb
+                gz, gb, grads[2 * layer] = output_backward(gz, ws[layer], hs[layer])
+                continue
             grads[2 * layer], grads[2 * layer + 1] = _split_k_wgrad(gz, hs[layer]), gb
             if layer == 0:
                 break
@@ -237,6 +244,9 @@ class _TanhMLP(torch.autograd.Function):
 # (hipBLASLt GEMMs + the one-pass HIP tanh backward: 3.99 s).  DESIGN.md §5.3 / §7,
 # profiles/r02_gemm_fused_bench.log, profiles/r02_ppo_sa_fused_vs_split_seeds.json.
 UPDATE_MLP = os.environ.get("VSS_UPDATE_MLP", "fused")
+# the fused path's output layer: "1" (default) = its backward and weight gradient in one streaming
+# pass (vss_output_backward), "0" = the padded backward + a split-K dW GEMM (A/B switch)
+OUTPUT_BWD = os.environ.get("VSS_OUTPUT_BWD", "1") == "1"
 
 
 def _fused_mlp_ok(seq: nn.Sequential) -> bool:

@@ -27,7 +27,8 @@ EXPORTED = ("vss_abi_version", "vss_error_string", "vss_step", "vss_step_replay"
             "vss_reset_dones_replay",
             "vss_compute_observations", "vss_mlp_packed_size", "vss_mlp_pack", "vss_policy_forward",
             "vss_value_forward_masked", "vss_episode_stats", "vss_tanh_grad_chunks", "vss_tanh_grad_bias",
-            "vss_linear_tanh", "vss_linear_tanh_backward_chunks", "vss_linear_tanh_backward")
+            "vss_linear_tanh", "vss_linear_tanh_backward_chunks", "vss_linear_tanh_backward",
+            "vss_output_backward_chunks", "vss_output_backward")
 
 
 class VssParams(ctypes.Structure):
@@ -116,6 +117,10 @@ def load() -> ctypes.CDLL:
     L.vss_linear_tanh_backward_chunks.restype = i64
     L.vss_linear_tanh_backward.argtypes = [P, i64, i32, i32, P, P, P, P, P]
     L.vss_linear_tanh_backward.restype = ctypes.c_int
+    L.vss_output_backward_chunks.argtypes = [i64, i32, i32]
+    L.vss_output_backward_chunks.restype = i64
+    L.vss_output_backward.argtypes = [P, i64, i32, i32, P, P, P, P, P, P]
+    L.vss_output_backward.restype = ctypes.c_int
     if L.vss_abi_version() != ABI_VERSION:
         raise NativeError(f"libvss_amd ABI {L.vss_abi_version()} != expected {ABI_VERSION}")
     _lib = L

@@ -4,13 +4,16 @@
     y = linear_tanh(x, w, b)                      # tanh(x @ w.T + b)
     gz, db = linear_tanh_backward(gz_next, w_next, y)
                                                   # gz = (gz_next @ w_next) * (1 - y^2), db = gz.sum(0)
+    gz, db, dw = output_backward(g_out, w_out, y) # the same through the output layer, plus its
+                                                  # weight gradient dw = g_out.T @ y, in one pass
 
 They replace what autograd issues for the Agent's nn.Linear -> nn.Tanh pairs
 (ppo_continuous_action_isaacgym.py:104-111): tanh_backward + the bias-gradient reduction
 (vss_tanh_grad_bias), addmm + tanh (vss_linear_tanh: one fp32 MFMA GEMM with bias and tanh in its
 epilogue), and the input-gradient GEMM of the layer above + tanh_backward + bias reduction
 (vss_linear_tanh_backward: one fp32 MFMA GEMM with the tanh derivative and the column sums in its
-epilogue).  On a ROCm device they run the HIP kernels (and raise if the library is missing); CPU
+epilogue), and for the output layer (1, 2 or 6 columns) that backward together with the output
+layer's weight gradient as one streaming pass over y (vss_output_backward).  On a ROCm device they run the HIP kernels (and raise if the library is missing); CPU
 tensors (the CPU test suite's PPO loop) take the same formulas in torch.
 """
 from __future__ import annotations
@@ -103,3 +106,42 @@ def linear_tanh_backward(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.T
                                          y.data_ptr(), gz.data_ptr(), partial.data_ptr()),
             "vss_linear_tanh_backward")
     return gz, partial.sum(0)
+
+
+def output_backward_ok(k_out: int, n: int) -> bool:
+    """Shapes vss_output_backward takes: k_out <= 8 output columns over a layer of width n | 1024."""
+    return 1 <= k_out <= 8 and n >= 128 and n % 128 == 0 and 1024 % n == 0
+
+
+def output_backward(g_out: torch.Tensor, w_out: torch.Tensor, y: torch.Tensor):
+    """Backward through the output nn.Linear (weight w_out (k_out, n)) into the tanh layer below it
+    (output y (rows, n), also the output layer's input), g_out (rows, k_out) the output's gradient:
+    gz = (g_out @ w_out) * (1 - y^2), db = gz.sum(0) and dw = g_out.T @ y (the output layer's weight
+    gradient)."""
+    if g_out.dim() != 2 or w_out.dim() != 2 or y.dim() != 2 or g_out.shape[0] != y.shape[0] \
+            or w_out.shape != (g_out.shape[1], y.shape[1]):
+        raise ValueError(f"output_backward: g_out {tuple(g_out.shape)}, w_out {tuple(w_out.shape)}, y {tuple(y.shape)}")
+    if g_out.device.type != "cuda":
+        gz = g_out.mm(w_out) * (1.0 - y * y)
+        return gz, gz.sum(0), g_out.t().mm(y)
+    rows, k_out = g_out.shape
+    n = y.shape[1]
+    _fp32_2d("vss_output_backward", g_out, w_out, y)
+    if not output_backward_ok(k_out, n):
+        raise ValueError(f"vss_output_backward: k_out <= 8 and n in (128, 256, 512, 1024) required, got {k_out}, {n}")
+    lib = N.load()
+    k_pad = 4 if k_out <= 4 else 8
+    gz = torch.empty((rows, n), device=y.device, dtype=torch.float32)
+    if rows == 0:
+        z = torch.zeros(n, device=y.device, dtype=torch.float32)
+        return gz, z, torch.zeros((k_out, n), device=y.device, dtype=torch.float32)
+    g_pad = torch.nn.functional.pad(g_out, (0, k_pad - k_out)).contiguous()
+    w_t = torch.nn.functional.pad(w_out, (0, 0, 0, k_pad - k_out)).t().contiguous()  # (n, k_pad)
+    y = y.contiguous()
+    chunks = lib.vss_output_backward_chunks(rows, k_pad, n)
+    bpart = torch.empty((chunks, n), device=y.device, dtype=torch.float32)
+    wpart = torch.empty((chunks, k_pad, n), device=y.device, dtype=torch.float32)
+    N.check(lib.vss_output_backward(N.stream_of(y.device), rows, k_pad, n, g_pad.data_ptr(), w_t.data_ptr(),
+                                    y.data_ptr(), gz.data_ptr(), bpart.data_ptr(), wpart.data_ptr()),
+            "vss_output_backward")
+    return gz, bpart.sum(0), wpart.sum(0)[:k_out]

@@ -1,13 +1,14 @@
 """PPO-update helpers (csrc/vss_update.hip): vss_tanh_grad_bias (one HIP pass for the backward of a
 hidden tanh layer) against torch's tanh_backward + bias-gradient reduction (the fp32 reference of
-the same op); the fused-epilogue GEMMs vss_linear_tanh / vss_linear_tanh_backward against torch
-fp32 and fp64; and the update's gradients through either path against plain autograd."""
+the same op); the fused-epilogue GEMMs vss_linear_tanh / vss_linear_tanh_backward and the output
+layer's one-pass backward vss_output_backward against torch fp32 and fp64; and the update's
+gradients through either path against plain autograd."""
 import pytest
 import torch
 
 import ppo_continuous_action_isaacgym as P
 from vss_amd import _native as N
-from vss_amd.update import linear_tanh, linear_tanh_backward, tanh_grad_bias
+from vss_amd.update import linear_tanh, linear_tanh_backward, output_backward, tanh_grad_bias
 
 from test_ppo import make_agent
 
@@ -144,6 +145,58 @@ def test_linear_tanh_backward_gpu(rows, k_next, n):
     torch.testing.assert_close(db.double(), ref.sum(0), rtol=1e-5, atol=1e-6 * scale * (rows ** 0.5 + 1))
     gz2, db2 = linear_tanh_backward(gn, wn, y)
     assert torch.equal(gz, gz2) and torch.equal(db, db2)
+
+
+def test_output_backward_cpu_formula_matches_autograd():
+    """output_backward's CPU form (what the CPU suite's PPO loop runs) against autograd through
+    Linear(n -> k_out) over tanh: the hidden pre-activation gradient, its bias and the output dW."""
+    g = torch.Generator().manual_seed(5)
+    z = torch.randn(33, 128, generator=g, dtype=torch.float64, requires_grad=True)
+    w = torch.randn(2, 128, generator=g, dtype=torch.float64, requires_grad=True)
+    y = torch.tanh(z)
+    out = y @ w.t()
+    gout = torch.randn(33, 2, generator=g, dtype=torch.float64)
+    gz_ref, gw_ref = torch.autograd.grad(out, [z, w], gout)
+    gz, db, dw = output_backward(gout, w.detach(), y.detach())
+    torch.testing.assert_close(gz, gz_ref)
+    torch.testing.assert_close(db, gz_ref.sum(0))
+    torch.testing.assert_close(dw, gw_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k_out,n", [(1, 256), (2, 256), (6, 256), (4, 128), (8, 512), (3, 1024)])
+@pytest.mark.parametrize("rows", [1, 3, 127, 4133, 70_000, 65_536])
+def test_output_backward_gpu(rows, k_out, n):
+    """vss_output_backward vs fp64: gz = (g_out @ w_out) * (1 - y^2), db = gz.sum(0), dw = g_out.T @ y;
+    deterministic (the same call twice gives the same bits)."""
+    g = torch.Generator(device="cuda").manual_seed(rows * 7 + k_out + n)
+    go = torch.randn(rows, k_out, device="cuda", generator=g) * 1e-2
+    wo = torch.randn(k_out, n, device="cuda", generator=g) * 0.1
+    y = torch.tanh(torch.randn(rows, n, device="cuda", generator=g) * 2)
+    gz, db, dw = output_backward(go, wo, y)
+    ref = (go.double() @ wo.double()) * (1 - y.double() ** 2)
+    scale = float((go.double().abs() @ wo.double().abs()).max())
+    assert float((gz.double() - ref).abs().max()) < 1.2e-7 * 8 * scale + 1e-12
+    torch.testing.assert_close(db.double(), ref.sum(0), rtol=1e-5, atol=1e-6 * scale * (rows ** 0.5 + 1))
+    dw_ref = go.double().t() @ y.double()
+    wscale = float((go.double().abs().t() @ y.double().abs()).max())
+    torch.testing.assert_close(dw.double(), dw_ref, rtol=1e-5, atol=2e-7 * wscale * (rows ** 0.5 + 1) + 1e-12)
+    gz2, db2, dw2 = output_backward(go, wo, y)
+    assert torch.equal(gz, gz2) and torch.equal(db, db2) and torch.equal(dw, dw2)
+
+
+@pytest.mark.gpu
+def test_output_backward_refusals_gpu():
+    lib = N.load()
+    buf = torch.zeros(1 << 16, device="cuda")
+    p, s = buf.data_ptr(), N.stream_of(buf.device)
+    assert lib.vss_output_backward_chunks(4, 4, 384) == -1  # 1024 % n
+    assert lib.vss_output_backward_chunks(4, 6, 256) == -1  # k_pad in {4, 8}
+    assert lib.vss_output_backward_chunks(4, 4, 256) > 0
+    assert lib.vss_output_backward(s, 4, 4, 256, p, p, p, p, p, None) != 0
+    assert lib.vss_output_backward(s, 4, 4, 256, p + 4, p, p, p, p, p) != 0  # misaligned
+    with pytest.raises(ValueError):
+        output_backward(buf[:36].view(4, 9), buf[:9 * 256].view(9, 256), buf[:1024].view(4, 256))
 
 
 @pytest.mark.gpu

@@ -736,6 +736,84 @@ static int launch(void* stream, const GemmArgs& a0, const Plan& pl) {
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 
+// ---- the first hidden layer's forward: y = tanh(x W^T + b), K = 52 (<= 64), N = 256 --------------
+// At 2,097,152 rows this is 0.44 GB in, 2.1 GB out and 56 GFLOP: the K loop is two K tiles and the
+// epilogue writes 8x what the loop reads, and the tiled GEMM ran them back to back (0.93-1.15 ms).
+// Here W^T (K x 256, <= 64 KB) is staged into LDS once per block and every wave works alone on
+// 32-row slabs: its x values straight from global memory (one float4 per lane and 8-wide K step),
+// 8 column tiles x 4 K steps of v_mfma_f32_32x32x2_f32 per float4, then bias + tanh and the stores;
+// with no barrier after the staging, one wave's tanh and stores run beside the other waves' MFMAs.
+// MFMA step (j, s): lane half h contributes k = 8j + 4h + s.
+constexpr int kFlThreads = 256;
+#ifndef VSS_LT_FIRST
+#define VSS_LT_FIRST 1  // profiling knob: 0 = the first layer on the tiled GEMM
+#endif
+
+static bool first_layer_ok(int32_t k, int32_t n) { return VSS_LT_FIRST && n == 256 && k % 4 == 0 && k > 48 && k <= 64; }
+
+template <int J>
+__global__ __launch_bounds__(kFlThreads, 2) void first_layer_kernel(int64_t rows, int k, const float* __restrict__ x,
+                                                                    const float* __restrict__ w,
+                                                                    const float* __restrict__ bias,
+                                                                    float* __restrict__ y) {
+  // wl[((kk * 2 + c) * 32 + r) * 4 + q] = w[32 (4c + q) + r][kk] (zero for kk >= k): a lane's 8 column
+  // tiles of one K row are two consecutive float4s, consecutive lanes 16 B apart
+  __shared__ float4 wl[8 * J * 2 * 32];
+  for (int i = threadIdx.x; i < 8 * J * 256; i += kFlThreads) {
+    const int q = i & 3, rr = (i >> 2) & 31, c = (i >> 7) & 1, kk = i >> 8;
+    reinterpret_cast<float*>(wl)[i] = kk < k ? w[(int64_t)(32 * (4 * c + q) + rr) * k + kk] : 0.0f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  float bcol[8];
+#pragma unroll
+  for (int ct = 0; ct < 8; ++ct) bcol[ct] = bias[ct * 32 + r];
+  const int64_t slabs = (rows + 31) / 32, step = (int64_t)gridDim.x * (kFlThreads / 64);
+  auto load_x = [&](int64_t sl, float4 (&xv)[J]) __attribute__((always_inline)) {
+    const int64_t row = sl * 32 + r;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int kk = 8 * j + 4 * h;
+      xv[j] = (row < rows && kk < k) ? *reinterpret_cast<const float4*>(x + row * k + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  // (Measured and not kept, profiles/r02_gemm_first_layer*.log: a software pipeline running one half
+  // slab's MFMAs beside the other half's epilogue -- both accumulator sets, so one wave per SIMD:
+  // 899 vs 804 us; the second block of each CU started half a slab late: no change.)
+  int64_t sl = (int64_t)blockIdx.x * (kFlThreads / 64) + wv;
+  float4 xv[J];
+  if (sl < slabs) load_x(sl, xv);
+  for (; sl < slabs; sl += step) {
+    float4 xc[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) xc[j] = xv[j];
+    if (sl + step < slabs) load_x(sl + step, xv);  // the next slab's x lands during this slab
+    f32x16 acc[8];
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct)
+      acc[ct] = (f32x16){0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const float av = s4 == 0 ? xc[j].x : s4 == 1 ? xc[j].y : s4 == 2 ? xc[j].z : xc[j].w;
+        const float4* wr = wl + ((8 * j + 4 * h + s4) * 2) * 32 + r;
+        const float4 b0 = wr[0], b1 = wr[32];
+        const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int ct = 0; ct < 8; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[ct], acc[ct], 0, 0, 0);
+      }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int64_t orow = sl * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (orow < rows) {
+#pragma unroll
+        for (int ct = 0; ct < 8; ++ct) y[orow * 256 + ct * 32 + r] = tanh_f32(acc[ct][e] + bcol[ct]);
+      }
+    }
+  }
+}
+
 // ---- the output layer's backward: k_next = 4 or 8 (the 1, 2 or 6 output columns, zero-padded) ------
 // gz = (gz_next W_next) * (1 - y^2) with a contraction of 4 or 8 is a streaming pass over y and gz
 // (2 x 4 B per element, ~2 k FLOP per element), not a GEMM: on the masked MFMA path it padded K to
@@ -893,6 +971,18 @@ int vss_linear_tanh(void* stream, int64_t rows, int32_t k_in, int32_t n_out, con
   if (!vgemm::shape_ok(rows, k_in, n_out) || misaligned(x) || misaligned(w) || misaligned(y) || !bias)
     return VSS_E_ARG;
   if (rows == 0) return VSS_OK;
+  if (vgemm::first_layer_ok(k_in, n_out)) {
+    const int64_t slabs = (rows + 31) / 32, per_block = vgemm::kFlThreads / 64;
+    int64_t g = (slabs + per_block - 1) / per_block;
+    if (g > 2 * vgemm::kGridCus) g = 2 * vgemm::kGridCus;  // two blocks (two waves per SIMD) per CU
+    if (k_in > 56)
+      hipLaunchKernelGGL(vgemm::first_layer_kernel<8>, dim3((unsigned)g), dim3(vgemm::kFlThreads), 0, (hipStream_t)stream,
+                         rows, k_in, x, w, bias, y);
+    else
+      hipLaunchKernelGGL(vgemm::first_layer_kernel<7>, dim3((unsigned)g), dim3(vgemm::kFlThreads), 0, (hipStream_t)stream,
+                         rows, k_in, x, w, bias, y);
+    return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+  }
   const vgemm::GemmArgs a{rows, n_out, k_in, x, w, bias, nullptr, y, nullptr, 0};
   return vgemm::launch<vgemm::EPI_TANH>(stream, a, vgemm::plan(rows, k_in, n_out, true));
 }

@@ -91,7 +91,7 @@ def test_update_mlp_paths_cpu_match_autograd(mlp, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,n", [(52, 256), (256, 512), (512, 512), (512, 256), (8, 128)])
+@pytest.mark.parametrize("k,n", [(52, 256), (256, 512), (512, 512), (512, 256), (8, 128), (56, 256), (64, 256)])
 @pytest.mark.parametrize("rows", [1, 127, 129, 4133, 70_000, 65_536])  # 65,536: exact shape, 4+ tiles per block
 def test_linear_tanh_gpu(rows, k, n):
     """vss_linear_tanh vs the fp32 torch op (addmm + tanh) and an fp64 reference: the fused GEMM

@@ -640,6 +640,9 @@ constexpr int kGridCus = 256;
 #define VSS_LT_CFG 256  // 256: 256 x 256 blocks for masked shapes with n % 256 == 0; 128: always 128 x 128
 #endif
 
+#ifndef VSS_LT_FWDCFG
+#define VSS_LT_FWDCFG 0  // profiling knob: forward exact shapes on 3 = 256 x 128 / 2 = 128 x 256 blocks (8 waves of 64 x 64)
+#endif
 #ifndef VSS_LT_BWDCFG
 #define VSS_LT_BWDCFG 0  // backward exact shapes: 0 = 128 x 128 blocks, 2 = 128 x 256, 3 = 256 x 128
 #endif
@@ -664,6 +667,12 @@ static Plan plan(int64_t rows, int32_t k, int32_t n, bool forward) {
   if (VSS_LT_D2CFG == 256 && VSS_LT_DEPTH == 2 && forward && exact && rows % Cfg256::BM == 0 && k % (2 * kKS) == 0 &&
       n % 256 == 0)
     pl.kind = 1;
+  if (VSS_LT_FWDCFG == 2 && VSS_LT_DEPTH == 2 && forward && exact && rows % Cfg128x256::BM == 0 && k % (2 * kKS) == 0 &&
+      n % Cfg128x256::BN == 0)
+    pl.kind = 2;
+  if (VSS_LT_FWDCFG == 3 && VSS_LT_DEPTH == 2 && forward && exact && rows % Cfg256x128::BM == 0 && k % (2 * kKS) == 0 &&
+      n % Cfg256x128::BN == 0)
+    pl.kind = 3;
   if (VSS_LT_BWDCFG == 2 && VSS_LT_DEPTH == 2 && !forward && exact && rows % Cfg128x256::BM == 0 && k % (2 * kKS) == 0 &&
       n % Cfg128x256::BN == 0)
     pl.kind = 2;
@@ -698,13 +707,13 @@ static bool shape_ok(int64_t rows, int32_t k, int32_t n) {
 template <int EPI, bool EXACT>
 static void launch_kind(const GemmArgs& a, const Plan& pl, hipStream_t s) {
   const dim3 grid((unsigned)pl.grid);
-  if constexpr (EPI == EPI_DTANH && EXACT) {
+  if constexpr (EXACT) {
     if (pl.kind == 2) {
-      hipLaunchKernelGGL((gemm_kernel_d2<EPI_DTANH, Cfg128x256>), grid, dim3(Cfg128x256::THREADS), 0, s, a);
+      hipLaunchKernelGGL((gemm_kernel_d2<EPI, Cfg128x256>), grid, dim3(Cfg128x256::THREADS), 0, s, a);
       return;
     }
     if (pl.kind == 3) {
-      hipLaunchKernelGGL((gemm_kernel_d2<EPI_DTANH, Cfg256x128>), grid, dim3(Cfg256x128::THREADS), 0, s, a);
+      hipLaunchKernelGGL((gemm_kernel_d2<EPI, Cfg256x128>), grid, dim3(Cfg256x128::THREADS), 0, s, a);
       return;
     }
   }

@@ -157,6 +157,10 @@ typedef struct vss_replay_draws {
 /* ABI version (VSS_ABI_VERSION). */
 int vss_abi_version(void);
 
+/* The build's source stamp: 16 hex digits of sha256 over the library's sources (csrc/Makefile
+ * STAMPED).  The Python loader recomputes it from the tree and refuses a stale library. */
+const char* vss_source_hash(void);
+
 /* Human-readable text for a VSS_E_* code. */
 const char* vss_error_string(int code);
 

@@ -22,50 +22,21 @@
 
 #pragma clang fp contract(off)
 
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "vss_step.hip targets gfx950 (CDNA4) only: wait_loads() and v_permlane32_swap are gfx950 encodings"
+#endif
+
 namespace vss {
 
 constexpr int kWave = 64;
-// Fields per step/rollout wave (one wave per workgroup; all 64 lanes take part in the streams),
-// per contract.  32, not 64: at 65,536 fields that is 2,048 waves = 2 per SIMD, so one wave's
-// physics overlaps the other wave's stores, and lanes L and L + 32 share a field, splitting its
-// per-robot physics (physics_split).  Measured (tools/ablate.py, profiles/r01_ablate_*):
-// FULL 48.8 -> 42.7 us with 32 fields per wave, -> 40.8 us with the split; SA 27.2 -> 25.9 us.
-// 16 and 24 are slower (LDS and VGPRs allow fewer than 3 waves per SIMD: the grid no longer fits
-// in one round).
-#ifndef VSS_FPW_FULL
-#define VSS_FPW_FULL 32
-#endif
-#ifndef VSS_FPW_SA
-#define VSS_FPW_SA 32
-#endif
-#ifndef VSS_FPW_CMA
-#define VSS_FPW_CMA 32
-#endif
-#ifndef VSS_FPW_DMA
-#define VSS_FPW_DMA 32
-#endif
-// Persistent step kernel (profiling knob, off in the product): at most VSS_STEP_GRID waves, each
-// walking batches w, w + G, ... with the next batch's inputs loaded during this batch's compute.
-// Measured at 65,536 fields (profiles/r02_ablate_persist_*.log): 1,024 waves x 2 batches is 12-33 %
-// SLOWER than 2,048 waves x 1 batch (FULL 45.3 vs 39.4 us, SA 33.2 vs 24.5 us): the second wave per
-// SIMD hides the load -> physics -> store latency chain better than in-wave prefetching does, and
-// on gfx9 a wave cannot consume a load issued after its previous stores without draining them.
-#ifndef VSS_STEP_PERSIST
-#define VSS_STEP_PERSIST 0
-#endif
-#ifndef VSS_STEP_GRID
-#define VSS_STEP_GRID 1024
-#endif
-constexpr bool kStepPersist = VSS_STEP_PERSIST != 0;
-template <int MODE>
-constexpr int fields_per_wave() {
-  return MODE == VSS_MODE_FULL ? VSS_FPW_FULL
-         : MODE == VSS_MODE_SA ? VSS_FPW_SA
-         : MODE == VSS_MODE_CMA ? VSS_FPW_CMA : VSS_FPW_DMA;
-}
-constexpr int kFpwRollout = VSS_FPW_FULL;  // the rollout kernel runs the FULL contract
-static_assert(fields_per_wave<0>() <= kWave && fields_per_wave<1>() <= kWave && fields_per_wave<2>() <= kWave &&
-              fields_per_wave<3>() <= kWave, "fields per wave");
+// Fields per step/rollout wave (one wave per workgroup; all 64 lanes take part in the streams).
+// 32, not 64: at 65,536 fields that is 2,048 waves = 2 per SIMD, so one wave's physics overlaps the
+// other wave's stores, and lanes L and L + 32 share a field, splitting its per-robot physics
+// (physics_split).  Measured (profiles/r01_ablate_*): FULL 48.8 -> 42.7 us with 32 fields per wave,
+// -> 40.8 us with the split; SA 27.2 -> 25.9 us.  16 and 24 are slower (profiles/r02_ablate_fields_
+// per_wave_*: LDS and VGPRs allow fewer than 3 waves per SIMD).  A persistent variant (1,024 waves x
+// 2 batches, next batch prefetched) was 12-33 % slower (profiles/r02_ablate_persist_*.log).
+constexpr int kFpw = 32;
 constexpr int kRec = 59;  // LDS floats per field record (58 used, odd stride: no bank conflicts)
 
 // ---- model constants (reference values cited in oracle/vss_oracle.c) --------
@@ -226,25 +197,6 @@ __device__ __forceinline__ float logf_poly(float x) {
   return (float)e * 0.69314718f + s * p;
 }
 
-// ---- diagnostic-only phase stamps (tools/ablate.py builds with -DVSS_PROF_STAMPS; never in the
-// product): s_memtime deltas per physics phase, summed per wave, added to g_prof by lane 0 ----------
-#ifdef VSS_PROF_STAMPS
-__device__ unsigned long long g_prof[8];
-__device__ __forceinline__ unsigned long long stamp() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-#define PROF_DECL unsigned long long prof_t = stamp(), prof_acc[5] = {0, 0, 0, 0, 0};
-#define PROF_MARK(k) { unsigned long long t_ = stamp(); prof_acc[k] += t_ - prof_t; prof_t = t_; }
-#define PROF_FLUSH if (threadIdx.x == 0) { for (int k_ = 0; k_ < 5; ++k_) atomicAdd(&g_prof[k_], prof_acc[k_]); }
-#else
-#define PROF_DECL
-#define PROF_MARK(k)
-#define PROF_FLUSH
-#endif
 
 // ---- per-field body state in registers ---------------------------------------------------------
 struct Bodies {
@@ -385,50 +337,6 @@ __device__ __forceinline__ void integrate_robot(float& x, float& y, float vx, fl
   s = 2.0f * qw * qz;
 }
 
-__device__ __forceinline__ void physics(Bodies& b, const float a[12]) {
-  PROF_DECL
-  float tl[6], tr[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    tl[i] = (a[2 * i] * K_WHEEL_RAD_S) * K_WHEEL_R;
-    tr[i] = (a[2 * i + 1] * K_WHEEL_RAD_S) * K_WHEEL_R;
-    heading(b, i);
-  }
-#pragma unroll 1
-  for (int sub = 0; sub < NSUB; ++sub) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) drive_robot(b.c[i], b.s[i], b.vx[i], b.vy[i], b.w[i], tl[i], tr[i]);
-    PROF_MARK(0)
-    b.bvx = b.bvx * K_BALL_DAMP;
-    b.bvy = b.bvy * K_BALL_DAMP;
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-      integrate_robot(b.x[i], b.y[i], b.vx[i], b.vy[i], b.w[i], b.qz[i], b.qw[i], b.c[i], b.s[i]);
-    b.bx = b.bx + b.bvx * K_H;
-    b.by = b.by + b.bvy * K_H;
-    PROF_MARK(1)
-#ifndef VSS_PROF_SKIP_RR
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = i + 1; j < 6; ++j) contact_robot_robot(b, i, j);
-#endif
-    PROF_MARK(2)
-#ifndef VSS_PROF_SKIP_BR
-#pragma unroll
-    for (int i = 0; i < 6; ++i) contact_ball_robot(b, i);
-#endif
-    PROF_MARK(3)
-#ifndef VSS_PROF_SKIP_WALLS
-#pragma unroll
-    for (int i = 0; i < 6; ++i) contact_walls(b.x[i], b.y[i], b.vx[i], b.vy[i], K_ROBOT_R);
-    contact_walls(b.bx, b.by, b.bvx, b.bvy, K_BALL_R);
-#endif
-    PROF_MARK(4)
-  }
-  PROF_FLUSH
-}
-
 // Both lane halves of a wave hold the same field (lane L and L + 32).  The per-robot phases
 // (drive, integration, walls) run on the half's own robots (lower half 0-2, upper half 3-5), and
 // one v_permlane32_swap per value writes robot k and k + 3 back into every lane's canonical
@@ -477,17 +385,12 @@ __device__ __forceinline__ void physics_split(Bodies& b, const float a[12]) {
     b.bvy = b.bvy * K_BALL_DAMP;
     b.bx = b.bx + b.bvx * K_H;
     b.by = b.by + b.bvy * K_H;
-#ifndef VSS_PROF_SKIP_RR
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
       for (int j = i + 1; j < 6; ++j) contact_robot_robot(b, i, j);
-#endif
-#ifndef VSS_PROF_SKIP_BR
 #pragma unroll
     for (int i = 0; i < 6; ++i) contact_ball_robot(b, i);
-#endif
-#ifndef VSS_PROF_SKIP_WALLS
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       ox[k] = up ? b.x[k + 3] : b.x[k];
@@ -501,15 +404,6 @@ __device__ __forceinline__ void physics_split(Bodies& b, const float a[12]) {
       exch(ovy[k], b.vy[k], b.vy[k + 3]);
     }
     contact_walls(b.bx, b.by, b.bvx, b.bvy, K_BALL_R);
-#else
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      ox[k] = up ? b.x[k + 3] : b.x[k];
-      oy[k] = up ? b.y[k + 3] : b.y[k];
-      ovx[k] = up ? b.vx[k + 3] : b.vx[k];
-      ovy[k] = up ? b.vy[k + 3] : b.vy[k];
-    }
-#endif
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -528,27 +422,13 @@ __device__ __forceinline__ void wait_loads() { __builtin_amdgcn_s_waitcnt(0x0F70
 // plus the lane's 32-bit byte offset, so they compile to `global_load/store v, v_off, s[base]`.
 // Written as one int64 index (ch * n + f0 + fl) the compiler formed every address per lane with two
 // quarter-rate v_mad_u64_u32 (the multiply by n fused into the divergent add): 46 channel loads and
-// 46 stores, ~400 VALU slots per wave.  uni() launders the base through readfirstlane so it is not
-// re-associated with the lane offset.
-#ifndef VSS_UNI
-#define VSS_UNI 0  // profiling knob: 1 = bases laundered through readfirstlane (measured ~1 us slower per step)
-#endif
-#ifndef VSS_BODY_WALK
-#define VSS_BODY_WALK 1  // profiling knob: 0 = state channels addressed as st[ch * n + f]
-#endif
-template <class T>
-__device__ __forceinline__ T* uni(T* p) {
-  if (!VSS_UNI) return p;
-  const uint64_t v = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
-}
+// 46 stores, ~400 VALU slots per wave.  (Laundering the base through readfirstlane spilled SGPRs and
+// measured ~1 us slower per step, profiles/r02_ablate_addressing.log.)
 // element at (wave-uniform base) + byte offset
 template <class T>
 __device__ __forceinline__ T& at(T* base, uint32_t byte_off) {
   using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
-  return *reinterpret_cast<T*>(reinterpret_cast<B*>(uni(base)) + byte_off);
+  return *reinterpret_cast<T*>(reinterpret_cast<B*>(base) + byte_off);
 }
 
 // fields f0 + fl (f0 wave-uniform).  The channels are walked with one running per-lane pointer
@@ -559,7 +439,7 @@ __device__ __forceinline__ void load_bodies(const float* __restrict__ st, int64_
 #pragma unroll
   for (int c = 0; c < VSS_STATE_CHANNELS; ++c) {
     if (c < VSS_CH_RQX || c >= VSS_CH_RQZ)  // the quaternions' x, y channels are not live (planar)
-      v[c] = VSS_BODY_WALK ? *q : st[c * n + f0 + fl];
+      v[c] = *q;
     q += n;
   }
   b.bx = v[VSS_CH_BALL_X]; b.by = v[VSS_CH_BALL_Y]; b.bvx = v[VSS_CH_BALL_VX]; b.bvy = v[VSS_CH_BALL_VY];
@@ -581,7 +461,7 @@ __device__ __forceinline__ void store_bodies(float* __restrict__ st, int64_t n, 
   float* q = st + f0 + fl;
 #pragma unroll
   for (int c = 0; c < VSS_STATE_CHANNELS; ++c) {
-    if (c < VSS_CH_RQX || c >= VSS_CH_RQZ) (VSS_BODY_WALK ? *q : st[c * n + f0 + fl]) = v[c];
+    if (c < VSS_CH_RQX || c >= VSS_CH_RQZ) *q = v[c];
     q += n;
   }
 }
@@ -989,9 +869,9 @@ __device__ __forceinline__ void ou_noise_split(float a[12], uint32_t k0, uint32_
 }
 
 // ---- the step kernel -------------------------------------------------------------------------------
-// One batch's inputs (kFpw fields of one wave), loaded into registers one batch ahead: the field's
-// bookkeeping and 46 live state channels, and the wave's contiguous AoS blocks of the batch's
-// 12-float action rows (FULL) or OU buffer rows (wrapped) and learner action rows (wrapped).
+// One wave's inputs (kFpw fields), all issued at the start of the kernel: the field's bookkeeping and
+// 46 live state channels, and the wave's contiguous AoS blocks of the batch's 12-float action rows
+// (FULL) or OU buffer rows (wrapped) and learner action rows (wrapped).
 struct BatchIn {
   int64_t progress, reset_prev;
   uint32_t ctr;
@@ -1030,262 +910,192 @@ __device__ __forceinline__ void load_batch(const StepArgs& args, int64_t f0, int
   if constexpr (MODE != VSS_MODE_FULL) prefetch_lrn<NL>(args.io.actions + f0 * NL, nv, lane, in.lrn);
 }
 
-#ifdef VSS_STEP_WPE  // profiling knob: minimum waves per SIMD the register allocation must allow
-#define VSS_STEP_ATTR __attribute__((amdgpu_waves_per_eu(VSS_STEP_WPE)))
-#else
-#define VSS_STEP_ATTR
-#endif
 template <int MODE, bool REPLAY = false>
-__global__ __launch_bounds__(kWave) VSS_STEP_ATTR void step_kernel(StepArgs args) {
+__global__ __launch_bounds__(kWave) void step_kernel(StepArgs args) {
   constexpr int A = MODE == VSS_MODE_FULL ? 6 : (MODE == VSS_MODE_DMA ? 3 : 1);
   constexpr int R = MODE == VSS_MODE_DMA ? 3 : 1;
   constexpr int NL = MODE == VSS_MODE_SA ? 2 : 6;  // learner action floats per field
-  constexpr int kFpw = fields_per_wave<MODE>();
-  // <= 32 fields per wave: lanes L and L + 32 hold field L (physics_split); lanes < 32 address the
-  // LDS records, so LDS holds 32 plain records or kFpw observation records, whichever is larger
-  constexpr bool kSplit = 2 * kFpw <= kWave;
-  constexpr int kLds = kSplit ? (32 * kRec > kFpw * obs_rec<A>() ? 32 * kRec : kFpw * obs_rec<A>()) : kWave * kRec;
+  // lanes L and L + 32 hold field L (physics_split); lanes < 32 address the LDS records, so LDS holds
+  // 32 plain records or kFpw observation records, whichever is larger
+  static_assert(2 * kFpw == kWave, "two lanes per field");
+  constexpr int kLds = 32 * kRec > kFpw * obs_rec<A>() ? 32 * kRec : kFpw * obs_rec<A>();
   static_assert(kFpw * obs_rec<A>() <= kLds, "observation records must fit the LDS block");
   __shared__ float lds[kLds + kTabWords];
   uint32_t* tab = reinterpret_cast<uint32_t*>(lds + kLds);
   stage_obs_table(tab, threadIdx.x);
-#ifdef VSS_PROF_STAGGER  // profiling knob: odd waves start VSS_PROF_STAGGER x 64 x 64 cycles late
-  if (blockIdx.x & 1)
-    for (int i = 0; i < VSS_PROF_STAGGER; ++i) __builtin_amdgcn_s_sleep(64);
-#endif
-#ifdef VSS_PRIO_HALF  // profiling knob: the first half of the grid (each SIMD's first wave) runs at raised priority
-  if (blockIdx.x < gridDim.x / 2) __builtin_amdgcn_s_setprio(VSS_PRIO_HALF);
-#endif
-#ifdef VSS_PROF_STAGGER_HALF  // profiling knob: the second half of the grid (dispatched as each SIMD's
-  // second wave) starts VSS_PROF_STAGGER_HALF x 16 x 64 cycles late
-  if (blockIdx.x >= gridDim.x / 2)
-    for (int i = 0; i < VSS_PROF_STAGGER_HALF; ++i) __builtin_amdgcn_s_sleep(16);
-#endif
 
   const int64_t n = args.n;
   const int lane = threadIdx.x;
-  const int fl = kSplit ? (lane & 31) : lane;  // this lane's field within the wave
-  const bool writer = !kSplit || lane < 32;    // writes the field's LDS record slots
+  const int fl = lane & 31;        // this lane's field within the wave
+  const bool writer = lane < 32;   // writes the field's LDS record slots
   const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
   float* rec = lds + fl * kRec;
   float* orec = lds + lane * obs_rec<A>();  // observation record (lanes < kFpw)
 
-  // Persistent over batches of kFpw fields: wave w advances batches w, w + G, w + 2G, ... (G =
-  // gridDim.x, sized by the host).  A batch's inputs are loaded one batch ahead (BatchIn), so they
-  // land while the wave computes the batch before, and the previous batch's stores drain behind this
-  // batch's compute (both are retired by the wait_loads() before this batch's first store).
-  const int64_t nbt = (n + kFpw - 1) / kFpw;
-  auto batch_nv = [&](int64_t t) { return (int)(n - t * kFpw < kFpw ? n - t * kFpw : kFpw); };
-  int64_t bt = blockIdx.x;
+  const int64_t f0 = (int64_t)blockIdx.x * kFpw;
+  const int nv = (int)(n - f0 < kFpw ? n - f0 : kFpw);
   BatchIn cur;
-  load_batch<MODE>(args, bt * kFpw, batch_nv(bt), fl, lane, cur);
-  for (;;) {
-    const int64_t f0 = bt * kFpw;
-    const int nv = batch_nv(bt);
-    const int64_t f = f0 + fl;
-    const bool valid = fl < nv;
-    const bool owner = valid && writer;  // stores the field's outputs
-    const int64_t btn = bt + gridDim.x;
-    const bool more = kStepPersist && btn < nbt;
-    BatchIn nxt;
-    if (more) load_batch<MODE>(args, btn * kFpw, batch_nv(btn), fl, lane, nxt);
+  load_batch<MODE>(args, f0, nv, fl, lane, cur);
+  const int64_t f = f0 + fl;
+  const bool valid = fl < nv;
+  const bool owner = valid && writer;  // stores the field's outputs
 
-    int64_t progress = cur.progress, reset_prev = cur.reset_prev;
-    uint32_t ctr = cur.ctr;
-    Bodies b = cur.b;
+  int64_t progress = cur.progress, reset_prev = cur.reset_prev;
+  uint32_t ctr = cur.ctr;
+  Bodies b = cur.b;
 
-    // -- actions: FULL reads (N,12); wrapped modes read + update the OU action buffer --------------
-    float a[12];
-    stage12(cur.blk, nv, lds, lane);
-    __syncthreads();
+  // -- actions: FULL reads (N,12); wrapped modes read + update the OU action buffer --------------
+  float a[12];
+  stage12(cur.blk, nv, lds, lane);
+  __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 12; ++k) a[k] = rec[k];
-    __syncthreads();
+  for (int k = 0; k < 12; ++k) a[k] = rec[k];
+  __syncthreads();
 
-    if constexpr (MODE != VSS_MODE_FULL) {
-      // random_ou (envs/wrappers.py:5-19): a <- clamp(a - 0.1 a + N(0, 0.15^2), -1, 1); the learner
-      // slots (pairs 0 for SA, 0..2 for CMA/DMA) are overwritten, so their normals are not needed.
-      constexpr int first_block = MODE == VSS_MODE_SA ? 0 : 1;
-      if constexpr (REPLAY) {
-        // torch.normal(0, 0.15, (N, 2, 3, 2)) of random_ou: the field's 12 recorded samples
-        if (valid) {
-          const float* z = args.rd.normals + f * 12;
+  if constexpr (MODE != VSS_MODE_FULL) {
+    // random_ou (envs/wrappers.py:5-19): a <- clamp(a - 0.1 a + N(0, 0.15^2), -1, 1); the learner
+    // slots (pairs 0 for SA, 0..2 for CMA/DMA) are overwritten, so their normals are not needed.
+    if constexpr (REPLAY) {
+      // torch.normal(0, 0.15, (N, 2, 3, 2)) of random_ou: the field's 12 recorded samples
+      if (valid) {
+        const float* z = args.rd.normals + f * 12;
 #pragma unroll
-          for (int k = NL; k < 12; ++k) a[k] = clampf((a[k] - K_OU_THETA * a[k]) + z[k], -1.0f, 1.0f);
-        }
-      } else if constexpr (kSplit) {
-        ou_noise_split<MODE>(a, k0, k1, (uint32_t)f, ctr);
-      } else {
-#pragma unroll
-        for (int blk = first_block; blk < 3; ++blk) {
-          uint32_t o[4];
-          philox(k0, k1, (uint32_t)f, ctr, kPurposeOU << 24, (uint32_t)blk, o);
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            int k = 4 * blk + 2 * h;
-            if (k < NL) continue;
-            float u1 = u01_open0(o[2 * h]);
-            float u2 = u01(o[2 * h + 1]);
-            float rad = sqrtf(-2.0f * logf_poly(u1));
-            float sz, cz;
-            sincos_turn(u2, sz, cz);
-            a[k] = clampf((a[k] - K_OU_THETA * a[k]) + K_OU_SIGMA * (rad * cz), -1.0f, 1.0f);
-            a[k + 1] = clampf((a[k + 1] - K_OU_THETA * a[k + 1]) + K_OU_SIGMA * (rad * sz), -1.0f, 1.0f);
-          }
-        }
-      }
-      stage_lrn<NL>(cur.lrn, nv, lds, lane);
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < NL; ++k) a[k] = rec[k];
-      __syncthreads();
-    }
-    float ou[12];
-    if constexpr (MODE != VSS_MODE_FULL) {
-#pragma unroll
-      for (int k = 0; k < 12; ++k) ou[k] = a[k];
-    }
-
-    // -- Ext VecTask.step clamp + pre_physics_step (envs/vss.py:180-187) -----------------------------
-    const float clip = args.p.clip_actions;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) a[k] = clampf(a[k], -clip, clip);
-    if (reset_prev != 0) progress = 0;
-
-    float pbx = b.bx, pby = b.by, prx[6], pry[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) { prx[i] = b.x[i]; pry[i] = b.y[i]; }
-
-    // -- gym.simulate replacement ------------------------------------------------------------------------
-#ifndef VSS_PROF_SKIP_PHYSICS  // profiling-only ablation knobs (tools/ablate.py); never set in the product
-    if (valid) {
-      if constexpr (kSplit) physics_split(b, a);
-      else physics(b, a);
-    }
-#endif
-
-#if defined(VSS_PRIO_HALF) && defined(VSS_PRIO_PHYS_ONLY)
-    __builtin_amdgcn_s_setprio(0);
-#endif
-    // -- post_physics_step: progress, rewards, dones (envs/vss.py:189-265) ----------------------------------
-    progress += 1;
-    float rew[24];
-    const int64_t done = rewards_and_done(args.p, b, pbx, pby, prx, pry, a, progress, rew);
-
-    // Retire every pending load here, before this batch's first store (the next batch's inputs, issued
-    // before this batch's compute, and so landed by now; the previous batch's stores drain with them):
-    // gfx9's vmcnt counts loads and stores, and the compiler can only wait for a load issued before
-    // stores by draining those stores too -- e.g. the rng counter, first used by the reset.
-    wait_loads();
-
-    // -- terminal observation (envs/vss.py:195-196) ----------------------------------------------------------
-    if (lane < kFpw) write_obs_record<A>(orec, b, a);
-    __syncthreads();
-#ifndef VSS_PROF_SKIP_OBS
-    coop_store_obs<A>(args.io.terminal_obs + f0 * (52 * A), nv, lds, tab, lane, MODE != VSS_MODE_FULL);
-#endif
-    __syncthreads();
-
-    // -- reset_dones (envs/vss.py:202, 267-333) ---------------------------------------------------------------
-    float dof[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) dof[k] = a[k];
-#ifndef VSS_PROF_SKIP_RESET
-    if (valid && done) {
-      const ResetDraws rd{k0, k1, (uint32_t)f, ctr, 0u, REPLAY ? args.rd.uniforms + f * args.rd.uniform_stride : nullptr,
-                          REPLAY ? args.rd_rounds : (uint32_t)kMaxRejectRounds};
-      if constexpr (kSplit) reset_field_split<REPLAY>(b, rd);
-      else reset_field<REPLAY>(b, rd);
-#pragma unroll
-      for (int k = 0; k < 12; ++k) dof[k] = dof[k] * 0.0f;
-    }
-#endif
-
-    // -- observation after reset (envs/vss.py:203) -------------------------------------------------------------
-    if (lane < kFpw) write_obs_record<A>(orec, b, dof);
-    __syncthreads();
-#ifndef VSS_PROF_SKIP_OBS
-    coop_store_obs<A>(args.io.obs + f0 * (52 * A), nv, lds, tab, lane, MODE != VSS_MODE_FULL || args.nt_obs != 0);
-#endif
-    __syncthreads();
-
-    // -- bookkeeping --------------------------------------------------------------------------------------------
-    const uint8_t time_out = (progress >= (int64_t)args.p.max_episode_length - 1) && done != 0;
-    if (owner) {
-      const uint32_t ufl = (uint32_t)fl;
-      store_bodies(args.s.state, n, f0, fl, b);
-      at(args.s.progress_buf + f0, 8u * ufl) = progress;
-      at(args.s.reset_buf + f0, 8u * ufl) = done;
-      at(args.s.rng_counter + f0, 4u * ufl) = ctr + 1u;
-#pragma unroll
-      for (int k = 0; k < R; ++k) {
-        at(args.io.time_outs + f0 * R, (uint32_t)(ufl * R + k)) = time_out;
-        at(args.io.progress_f + f0 * R, 4u * (ufl * R + k)) = (float)progress;
-      }
-      if constexpr (MODE == VSS_MODE_DMA) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) at(args.io.dones_rep + f0 * 3, 8u * (ufl * 3 + k)) = done;
-      }
-    }
-
-    // dof_velocity_buf (N,12) and, wrapped, the OU action buffer (zeroed for done fields)
-    if (writer) {
-#pragma unroll
-      for (int k = 0; k < 12; ++k) rec[k] = dof[k];
-    }
-    __syncthreads();
-    coop_store<12>(args.s.dof_velocity_buf + f0 * 12, nv, lds, lane);
-    __syncthreads();
-    if constexpr (MODE != VSS_MODE_FULL) {
-      if (writer) {
-#pragma unroll
-        for (int k = 0; k < 12; ++k) rec[k] = done ? ou[k] * 0.0f : ou[k];
-      }
-      __syncthreads();
-      coop_store<12>(args.io.ou_buf + f0 * 12, nv, lds, lane);
-      __syncthreads();
-    }
-
-    // rewards
-    if constexpr (MODE == VSS_MODE_FULL) {
-      if (writer) {
-#pragma unroll
-        for (int k = 0; k < 24; ++k) rec[k] = rew[k];
-      }
-      __syncthreads();
-      coop_store<24>(args.io.rew + f0 * 24, nv, lds, lane);
-      if (owner && args.io.reward_sum) at(args.io.reward_sum + f0, 4u * (uint32_t)fl) = ((rew[0] + rew[1]) + rew[2]) + rew[3];
-    } else if constexpr (MODE == VSS_MODE_SA) {
-      if (owner) {
-        at(reinterpret_cast<float4*>(args.io.rew) + f0, 16u * (uint32_t)fl) = make_float4(rew[0], rew[1], rew[2], rew[3]);
-        at(args.io.reward_sum + f0, 4u * (uint32_t)fl) = ((rew[0] + rew[1]) + rew[2]) + rew[3];
-      }
-    } else if constexpr (MODE == VSS_MODE_CMA) {
-      if (owner) {
-        float m[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) m[c] = ((rew[c] + rew[4 + c]) + rew[8 + c]) / 3.0f;
-        at(reinterpret_cast<float4*>(args.io.rew) + f0, 16u * (uint32_t)fl) = make_float4(m[0], m[1], m[2], m[3]);
-        at(args.io.reward_sum + f0, 4u * (uint32_t)fl) = ((m[0] + m[1]) + m[2]) + m[3];
+        for (int k = NL; k < 12; ++k) a[k] = clampf((a[k] - K_OU_THETA * a[k]) + z[k], -1.0f, 1.0f);
       }
     } else {
-      if (writer) {
-#pragma unroll
-        for (int k = 0; k < 12; ++k) rec[k] = rew[k];
-      }
-      __syncthreads();
-      coop_store<12>(args.io.rew + f0 * 12, nv, lds, lane);
-      if (owner) {
-#pragma unroll
-        for (int ag = 0; ag < 3; ++ag)
-          at(args.io.reward_sum + f0 * 3, 4u * ((uint32_t)fl * 3 + ag)) =
-              ((rew[4 * ag] + rew[4 * ag + 1]) + rew[4 * ag + 2]) + rew[4 * ag + 3];
-      }
+      ou_noise_split<MODE>(a, k0, k1, (uint32_t)f, ctr);
     }
-    if (!more) break;
-    __syncthreads();  // the next batch's LDS staging follows this batch's last LDS reads
-    cur = nxt;
-    bt = btn;
+    stage_lrn<NL>(cur.lrn, nv, lds, lane);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NL; ++k) a[k] = rec[k];
+    __syncthreads();
+  }
+  float ou[12];
+  if constexpr (MODE != VSS_MODE_FULL) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) ou[k] = a[k];
+  }
+
+  // -- Ext VecTask.step clamp + pre_physics_step (envs/vss.py:180-187) -----------------------------
+  const float clip = args.p.clip_actions;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) a[k] = clampf(a[k], -clip, clip);
+  if (reset_prev != 0) progress = 0;
+
+  float pbx = b.bx, pby = b.by, prx[6], pry[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) { prx[i] = b.x[i]; pry[i] = b.y[i]; }
+
+  // -- gym.simulate replacement ------------------------------------------------------------------------
+  if (valid) physics_split(b, a);
+
+  // -- post_physics_step: progress, rewards, dones (envs/vss.py:189-265) ----------------------------------
+  progress += 1;
+  float rew[24];
+  const int64_t done = rewards_and_done(args.p, b, pbx, pby, prx, pry, a, progress, rew);
+
+  // Retire every pending load here, before the first store: gfx9's vmcnt counts loads and stores, and
+  // the compiler can only wait for a load issued before stores by draining those stores too -- e.g.
+  // the rng counter, first used by the reset.
+  wait_loads();
+
+  // -- terminal observation (envs/vss.py:195-196) ----------------------------------------------------------
+  if (lane < kFpw) write_obs_record<A>(orec, b, a);
+  __syncthreads();
+  coop_store_obs<A>(args.io.terminal_obs + f0 * (52 * A), nv, lds, tab, lane, MODE != VSS_MODE_FULL);
+  __syncthreads();
+
+  // -- reset_dones (envs/vss.py:202, 267-333) ---------------------------------------------------------------
+  float dof[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) dof[k] = a[k];
+  if (valid && done) {
+    const ResetDraws rd{k0, k1, (uint32_t)f, ctr, 0u, REPLAY ? args.rd.uniforms + f * args.rd.uniform_stride : nullptr,
+                        REPLAY ? args.rd_rounds : (uint32_t)kMaxRejectRounds};
+    reset_field_split<REPLAY>(b, rd);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) dof[k] = dof[k] * 0.0f;
+  }
+
+  // -- observation after reset (envs/vss.py:203) -------------------------------------------------------------
+  if (lane < kFpw) write_obs_record<A>(orec, b, dof);
+  __syncthreads();
+  coop_store_obs<A>(args.io.obs + f0 * (52 * A), nv, lds, tab, lane, MODE != VSS_MODE_FULL || args.nt_obs != 0);
+  __syncthreads();
+
+  // -- bookkeeping --------------------------------------------------------------------------------------------
+  const uint8_t time_out = (progress >= (int64_t)args.p.max_episode_length - 1) && done != 0;
+  if (owner) {
+    const uint32_t ufl = (uint32_t)fl;
+    store_bodies(args.s.state, n, f0, fl, b);
+    at(args.s.progress_buf + f0, 8u * ufl) = progress;
+    at(args.s.reset_buf + f0, 8u * ufl) = done;
+    at(args.s.rng_counter + f0, 4u * ufl) = ctr + 1u;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      at(args.io.time_outs + f0 * R, (uint32_t)(ufl * R + k)) = time_out;
+      at(args.io.progress_f + f0 * R, 4u * (ufl * R + k)) = (float)progress;
+    }
+    if constexpr (MODE == VSS_MODE_DMA) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) at(args.io.dones_rep + f0 * 3, 8u * (ufl * 3 + k)) = done;
+    }
+  }
+
+  // dof_velocity_buf (N,12) and, wrapped, the OU action buffer (zeroed for done fields)
+  if (writer) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) rec[k] = dof[k];
+  }
+  __syncthreads();
+  coop_store<12>(args.s.dof_velocity_buf + f0 * 12, nv, lds, lane);
+  __syncthreads();
+  if constexpr (MODE != VSS_MODE_FULL) {
+    if (writer) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) rec[k] = done ? ou[k] * 0.0f : ou[k];
+    }
+    __syncthreads();
+    coop_store<12>(args.io.ou_buf + f0 * 12, nv, lds, lane);
+    __syncthreads();
+  }
+
+  // rewards
+  if constexpr (MODE == VSS_MODE_FULL) {
+    if (writer) {
+#pragma unroll
+      for (int k = 0; k < 24; ++k) rec[k] = rew[k];
+    }
+    __syncthreads();
+    coop_store<24>(args.io.rew + f0 * 24, nv, lds, lane);
+    if (owner && args.io.reward_sum) at(args.io.reward_sum + f0, 4u * (uint32_t)fl) = ((rew[0] + rew[1]) + rew[2]) + rew[3];
+  } else if constexpr (MODE == VSS_MODE_SA) {
+    if (owner) {
+      at(reinterpret_cast<float4*>(args.io.rew) + f0, 16u * (uint32_t)fl) = make_float4(rew[0], rew[1], rew[2], rew[3]);
+      at(args.io.reward_sum + f0, 4u * (uint32_t)fl) = ((rew[0] + rew[1]) + rew[2]) + rew[3];
+    }
+  } else if constexpr (MODE == VSS_MODE_CMA) {
+    if (owner) {
+      float m[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) m[c] = ((rew[c] + rew[4 + c]) + rew[8 + c]) / 3.0f;
+      at(reinterpret_cast<float4*>(args.io.rew) + f0, 16u * (uint32_t)fl) = make_float4(m[0], m[1], m[2], m[3]);
+      at(args.io.reward_sum + f0, 4u * (uint32_t)fl) = ((m[0] + m[1]) + m[2]) + m[3];
+    }
+  } else {
+    if (writer) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) rec[k] = rew[k];
+    }
+    __syncthreads();
+    coop_store<12>(args.io.rew + f0 * 12, nv, lds, lane);
+    if (owner) {
+#pragma unroll
+      for (int ag = 0; ag < 3; ++ag)
+        at(args.io.reward_sum + f0 * 3, 4u * ((uint32_t)fl * 3 + ag)) =
+            ((rew[4 * ag] + rew[4 * ag + 1]) + rew[4 * ag + 2]) + rew[4 * ag + 3];
+    }
   }
 }
 
@@ -1303,23 +1113,22 @@ struct RolloutArgs {
 };
 
 __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
-  static_assert(kFpwRollout * kRecObs6 <= kWave * kRec, "observation records must fit the LDS block");
+  static_assert(kFpw * kRecObs6 <= kWave * kRec, "observation records must fit the LDS block");
   __shared__ float lds[kWave * kRec + kTabWords];
   uint32_t* tab = reinterpret_cast<uint32_t*>(lds + kWave * kRec);
   stage_obs_table(tab, threadIdx.x);
   const int64_t n = args.n;
   const int lane = threadIdx.x;
-  constexpr bool kSplit = 2 * kFpwRollout == kWave;  // lanes L and L + 32 hold the same field
-  const int fl = kSplit ? (lane & (kFpwRollout - 1)) : lane;
-  const int64_t f0 = (int64_t)blockIdx.x * kFpwRollout;
-  const int nv = (int)(n - f0 < kFpwRollout ? n - f0 : kFpwRollout);
+  const int fl = lane & (kFpw - 1);  // lanes L and L + 32 hold the same field
+  const int64_t f0 = (int64_t)blockIdx.x * kFpw;
+  const int nv = (int)(n - f0 < kFpw ? n - f0 : kFpw);
   const int64_t f = f0 + fl;
   const bool valid = fl < nv;  // both halves carry the state (and apply resets) across steps
-  const bool owner = valid && lane < kFpwRollout;
-  const bool writer = lane < kFpwRollout;
+  const bool owner = valid && lane < kFpw;
+  const bool writer = lane < kFpw;
   const uint32_t k0 = (uint32_t)args.p.seed, k1 = (uint32_t)(args.p.seed >> 32);
   float* rec = lds + fl * kRec;
-  float* orec = lds + lane * kRecObs6;  // observation record (lanes < kFpwRollout)
+  float* orec = lds + lane * kRecObs6;  // observation record (lanes < kFpw)
 
   int64_t progress = 0, reset_prev = 0;
   uint32_t ctr = 0;
@@ -1351,8 +1160,7 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
 #pragma unroll
     for (int i = 0; i < 6; ++i) { prx[i] = b.x[i]; pry[i] = b.y[i]; }
     if (valid) {
-      if constexpr (kSplit) physics_split(b, a);
-      else physics(b, a);
+      physics_split(b, a);
     }
     progress += 1;
     float rew[24];
@@ -1362,7 +1170,7 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
     // this step's stores: the previous step's stores, issued before it, have drained behind the
     // physics, and the streams below leave no load pending (see wait_loads)
     wait_loads();
-    if (lane < kFpwRollout) write_obs_record<6>(orec, b, a);
+    if (lane < kFpw) write_obs_record<6>(orec, b, a);
     __syncthreads();
     coop_store_obs<6>(args.io.terminal_obs + (step_off + f0) * 312, nv, lds, tab, lane, true);  // K steps: past the cache
     __syncthreads();
@@ -1370,12 +1178,11 @@ __global__ __launch_bounds__(kWave) void rollout_kernel(RolloutArgs args) {
     for (int i = 0; i < 12; ++i) dof[i] = a[i];
     if (valid && done) {
       const ResetDraws rd{k0, k1, (uint32_t)f, ctr + (uint32_t)k, 0u, nullptr, (uint32_t)kMaxRejectRounds};
-      if constexpr (kSplit) reset_field_split<false>(b, rd);
-      else reset_field<false>(b, rd);
+      reset_field_split<false>(b, rd);
 #pragma unroll
       for (int i = 0; i < 12; ++i) dof[i] = dof[i] * 0.0f;
     }
-    if (lane < kFpwRollout) write_obs_record<6>(orec, b, dof);
+    if (lane < kFpw) write_obs_record<6>(orec, b, dof);
     __syncthreads();
     coop_store_obs<6>(args.io.obs + (step_off + f0) * 312, nv, lds, tab, lane, true);
     __syncthreads();
@@ -1496,10 +1303,13 @@ static int check_state(int64_t n, const vss_state* st) {
 
 static int launch_status() { return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH; }
 
+// Rejection rounds one replay row holds: (stride - 8) / 14.  A row with more rounds than the kernel
+// bounds (kMaxRejectRounds) is refused here rather than replayed short (the kernel would stop early
+// and read round draws as yaw draws).
 static int replay_rounds(const vss_replay_draws* d) {
   if (!d || bad(d->uniforms, 4) || d->uniform_stride < 22 || d->uniform_stride > (int64_t(1) << 20)) return -1;
   const int64_t r = (d->uniform_stride - 8) / 14;
-  return (int)(r < vss::kMaxRejectRounds ? r : vss::kMaxRejectRounds);
+  return r > vss::kMaxRejectRounds ? -1 : (int)r;
 }
 
 template <bool REPLAY>
@@ -1523,11 +1333,7 @@ static int step_impl(void* stream, int64_t n, int32_t mode, const vss_params* p,
   // the 256 MiB Infinity Cache (coop_store_obs)
   const uint32_t nt_obs = mode == VSS_MODE_FULL && n > (int64_t)(256ll << 20) / 3101 ? 1u : 0u;
   vss::StepArgs args{n, *p, *st, *io, REPLAY ? *rd : vss_replay_draws{}, (uint32_t)rounds, nt_obs};
-  const int fpw = mode == VSS_MODE_FULL ? vss::fields_per_wave<VSS_MODE_FULL>()
-                  : mode == VSS_MODE_SA ? vss::fields_per_wave<VSS_MODE_SA>()
-                  : mode == VSS_MODE_CMA ? vss::fields_per_wave<VSS_MODE_CMA>() : vss::fields_per_wave<VSS_MODE_DMA>();
-  const int64_t batches = (n + fpw - 1) / fpw;
-  const dim3 grid((unsigned)(vss::kStepPersist && batches > VSS_STEP_GRID ? VSS_STEP_GRID : batches)), block(vss::kWave);
+  const dim3 grid((unsigned)((n + vss::kFpw - 1) / vss::kFpw)), block(vss::kWave);
   hipStream_t s = (hipStream_t)stream;
   switch (mode) {
     case VSS_MODE_FULL: hipLaunchKernelGGL((vss::step_kernel<VSS_MODE_FULL, REPLAY>), grid, block, 0, s, args); break;
@@ -1542,15 +1348,6 @@ extern "C" {
 
 int vss_abi_version(void) { return VSS_ABI_VERSION; }
 
-#ifdef VSS_PROF_STAMPS
-// diagnostic builds only: copy (and clear) the 5 per-phase cycle sums
-int vss_prof_read(unsigned long long* host_out) {
-  unsigned long long zero[8] = {0};
-  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(vss::g_prof), sizeof(zero)) != hipSuccess) return VSS_E_LAUNCH;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(vss::g_prof), zero, sizeof(zero)) != hipSuccess) return VSS_E_LAUNCH;
-  return VSS_OK;
-}
-#endif
 
 const char* vss_error_string(int code) {
   switch (code) {
@@ -1580,7 +1377,7 @@ int vss_rollout(void* stream, int64_t n, int32_t k_steps, const vss_params* p, c
     return VSS_E_ARG;
   if (n == 0) return VSS_OK;
   vss::RolloutArgs args{n, k_steps, *p, *st, *io};
-  const dim3 grid((unsigned)((n + vss::kFpwRollout - 1) / vss::kFpwRollout)), block(vss::kWave);
+  const dim3 grid((unsigned)((n + vss::kFpw - 1) / vss::kFpw)), block(vss::kWave);
   hipLaunchKernelGGL(vss::rollout_kernel, grid, block, 0, (hipStream_t)stream, args);
   return launch_status();
 }

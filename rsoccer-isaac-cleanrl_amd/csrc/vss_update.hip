@@ -15,34 +15,19 @@
 
 #include "../../include/vss.h"
 
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "vss_update.hip targets gfx950 (CDNA4) only"
+#endif
+
 namespace vupd {
 
-// tuning knobs (tools/tanh_grad_bench.py builds variants; the product uses the defaults)
-#ifndef VSS_TG_U
-#define VSS_TG_U 8
-#endif
-#ifndef VSS_TG_WAVES
-#define VSS_TG_WAVES 4
-#endif
-#ifndef VSS_TG_MAXBLK
-#define VSS_TG_MAXBLK 2048
-#endif
-#ifndef VSS_TG_NT
-#define VSS_TG_NT 0
-#endif
 constexpr int kThreads = 256;
-constexpr int kU = VSS_TG_U;                   // rows per lane in flight (2 x kU 16-B loads before the first use)
-constexpr int64_t kMaxBlocks = VSS_TG_MAXBLK;  // the partial sums are (blocks x cols)
+constexpr int kU = 8;                  // rows per lane in flight (2 x kU 16-B loads before the first use)
+constexpr int kWavesPerSimd = 4;       // register budget: all 2 kU loads of a lane in flight
+constexpr int64_t kMaxBlocks = 2048;   // the partial sums are (blocks x cols)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 ld(const float4* p) {
-#if VSS_TG_NT
-  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-  return make_float4(v.x, v.y, v.z, v.w);
-#else
-  return *p;
-#endif
-}
+__device__ __forceinline__ float4 ld(const float4* p) { return *p; }
 
 __device__ __forceinline__ float4 tanh_grad(float4 g, float4 y) {
   // d tanh(z) / dz = 1 - tanh(z)^2
@@ -72,7 +57,7 @@ __host__ inline int64_t n_blocks(int64_t rows, int cols) {
 // effective); a two-register-set software pipeline compiled to a vmcnt(0) per tile and was no
 // faster.
 template <int C4>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, VSS_TG_WAVES))) void tanh_grad_bias_kernel(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, kWavesPerSimd))) void tanh_grad_bias_kernel(
     int64_t rows, const float4* __restrict__ gy, const float4* __restrict__ y, float4* __restrict__ gz,
     float4* __restrict__ partial) {
   constexpr int RG = kThreads / C4;
@@ -146,30 +131,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(1, VSS
 // epilogue goes through LDS so that global stores (and, backward, the y loads) are 16 B per lane.
 namespace vgemm {
 
-#ifndef VSS_LT_PERSIST
-#define VSS_LT_PERSIST 1
-#endif
-#ifndef VSS_LT_PROBE
-#define VSS_LT_PROBE 0
-#endif
-#ifndef VSS_LT_DEPTH
-#define VSS_LT_DEPTH 2  // 2: exact shapes with K % 64 == 0 on 128 x 128 blocks load two K tiles ahead
-#endif
-#ifndef VSS_LT_D2CFG
-#define VSS_LT_D2CFG 256  // 256: the forward's exact shapes with n % 256 == 0 run gemm_kernel_d2 on 256 x 256 blocks
-#endif
-#ifndef VSS_LT_PRIO
-#define VSS_LT_PRIO 0  // 1: gemm_kernel_d2 raises the wave priority over its MFMA phases
-#endif
-#ifndef VSS_LT_EXACT
-#define VSS_LT_EXACT 1  // unmasked loads for exact shapes
-#endif
-#ifndef VSS_LT_NOMASK
-#define VSS_LT_NOMASK 1  // 1: gemm_kernel_d2 (exact shapes only) stores its epilogue without row masks
-#endif
-#ifndef VSS_LT_STAGGER
-#define VSS_LT_STAGGER 0  // profiling knob: the second half of the grid starts this many 100-MHz ticks late
-#endif
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 enum { EPI_TANH = 0, EPI_DTANH = 1 };
@@ -182,12 +143,7 @@ __device__ __forceinline__ float tanh_f32(float z) {
   const float poly = z + z * s * (-0.333333343f + s * (0.133333340f + s * (-0.0539682545f + s * 0.0218694885f)));
   const float t = __builtin_amdgcn_exp2f(-2.8853900817779268f * a);
   const float ex = copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), z);
-#ifdef VSS_LT_TANH_FAST  // profiling knob: the exponential form only
-  (void)poly;
-  return ex;
-#else
   return a < 0.3f ? poly : ex;
-#endif
 }
 
 constexpr int kKS = 32, kLS = kKS + 4;  // K tile, LDS row stride (floats; conflict-free ds_read_b128 groups)
@@ -201,20 +157,17 @@ struct Cfg {
   static constexpr int WROWS = BM / WM, WCOLS = BN / WN;
   static constexpr int TM = WROWS / 32, TN = WCOLS / 32;
   static constexpr int LDSF = 2 * (BM + BN) * kLS;  // two K-tile buffers
-  // gemm_kernel_d2's epilogue scratch starts at K-tile buffer 1 and may run past it (8 waves of
-  // 64 x 64 on 128 x 256 blocks): the kernel's LDS is then sized to cover it
-  static constexpr int SCR = WM * WN * 32 * kES;
-  static constexpr int LDSA = LDSF + (SCR > (BM + BN) * kLS ? SCR - (BM + BN) * kLS : 0);
+  static constexpr int SCR = WM * WN * 32 * kES;  // epilogue scratch, inside K-tile buffer 1
+  static_assert(SCR <= (BM + BN) * kLS, "epilogue scratch must fit one K-tile buffer");
   static constexpr int LROWS = THREADS / 8;          // rows one staging pass covers (8 float4 per 32-float row)
   static constexpr int RA = BM / LROWS, RB = BN / LROWS;
-  static constexpr int BLOCKS_PER_CU = LDSA * 4 * 2 <= 160 * 1024 ? 2 : 1;
+  static constexpr int BLOCKS_PER_CU = LDSF * 4 * 2 <= 160 * 1024 ? 2 : 1;
   static_assert(WCOLS == 64, "the epilogue streams 64-column wave tiles");
   static_assert(RA * LROWS == BM && RB * LROWS == BN, "staging passes must tile the block");
 };
 using Cfg128 = Cfg<128, 128, 2, 2>;     // 4 waves, 72 KB LDS: two blocks per CU
 using Cfg256 = Cfg<256, 256, 2, 4>;     // 8 waves of 128 x 64, 144 KB LDS: one block per CU
-using Cfg128x256 = Cfg<128, 256, 2, 4>; // 8 waves of 64 x 64, 126 KB LDS: one block per CU
-using Cfg256x128 = Cfg<256, 128, 4, 2>; // 8 waves of 64 x 64, 126 KB LDS: one block per CU
+// (measured and not kept: 8-wave 256 x 128 / 128 x 256 blocks, profiles/r02_gemm_{fwd,bwd}_tiles*.log)
 
 struct GemmArgs {
   int64_t rows;
@@ -279,9 +232,6 @@ __device__ __forceinline__ void store_tile(const GemmArgs& p, f32x16 (&acc)[TM][
                         v.w * fmaf(-yq.w, yq.w, 1.0f));
         if (!MASK || row < M) vupd::add4(csum, v);
       }
-#if VSS_LT_PROBE == 5  // profiling knob: no global stores in the epilogue (values kept live; timing only)
-      asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-#else
       if (!MASK || row < M) {
         if constexpr (EPI == EPI_DTANH) {
           // the backward's gradient streams out nontemporally: 1-4 % faster on the three backward
@@ -292,7 +242,6 @@ __device__ __forceinline__ void store_tile(const GemmArgs& p, f32x16 (&acc)[TM][
           *reinterpret_cast<float4*>(p.out + row * p.n + colw + ec) = v;
         }
       }
-#endif
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -324,7 +273,6 @@ __device__ __forceinline__ void write_colsums(const GemmArgs& p, float4 csum, fl
 template <int EPI, class C, bool EXACT>
 __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(GemmArgs p) {
   constexpr int BM = C::BM, BN = C::BN, TM = C::TM, TN = C::TN, LROWS = C::LROWS;
-  static_assert(C::SCR <= (BM + BN) * kLS, "epilogue scratch must fit one K-tile buffer");
   __shared__ float lds[C::LDSF];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv / C::WN, wn = wv % C::WN;
   const int nb = p.n / BN;
@@ -412,32 +360,21 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(Gemm
       // the next K tile of the flat pipeline: this tile's kt + 1, else the next tile's first
       const bool last = kt + 1 == ktiles;
       const bool more = !last || has_next;
-#if VSS_LT_PROBE == 4  // profiling knob 4: no global loads in the K loop (stale staging, timing only)
-      if (last && has_next) set_fetch_tile(next);
-#else
       // one load site, no branch around it: the loaded registers then need no copies at a control
       // flow join (copies made the compiler wait for the loads before the MFMAs).  After the
       // block's last tile this re-fetches its first K tile, which is never written to LDS.
       if (last && has_next) set_fetch_tile(next);
       gload(ra, rb, last ? 0 : kt + 1);
       __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMAs (the scheduler sinks them)
-#endif
       const float* As = lds + buf * (BM + BN) * kLS + (wm * C::WROWS + r) * kLS + h * 16;
       const float* Bs = lds + buf * (BM + BN) * kLS + BM * kLS + (wn * C::WCOLS + r) * kLS + h * 16;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         float4 a4[TM], b4[TN];
-#if VSS_LT_PROBE == 1  // profiling knob: operands from registers only (no LDS reads in the K loop)
-#pragma unroll
-        for (int i = 0; i < TM; ++i) a4[i] = ra[i % C::RA];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) b4[j] = rb[j % C::RB];
-#else
 #pragma unroll
         for (int i = 0; i < TM; ++i) a4[i] = *reinterpret_cast<const float4*>(As + i * 32 * kLS + q * 4);
 #pragma unroll
         for (int j = 0; j < TN; ++j) b4[j] = *reinterpret_cast<const float4*>(Bs + j * 32 * kLS + q * 4);
-#endif
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -449,15 +386,11 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(Gemm
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
             }
       }
-#if VSS_LT_PROBE != 2  // profiling knob 2: no LDS staging / barrier (wrong results, timing only)
       if (more) {
         swrite(ra, rb, buf ^ 1);
-#if VSS_LT_PROBE != 3  // profiling knob 3: no barrier (wrong results, timing only)
         __syncthreads();
-#endif
         buf ^= 1;
       }
-#endif
     }
 
     // epilogue through the free LDS buffer (buf ^ 1: every wave has passed the barrier after its last read)
@@ -474,7 +407,7 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(Gemm
   }
 }
 
-// Exact shapes (rows % BM == 0, K % 64 == 0), loads TWO K tiles ahead (VSS_LT_DEPTH == 2): two
+// Exact shapes (rows % BM == 0, K % 64 == 0), loads TWO K tiles ahead: two
 // register sets alternate with the two LDS buffers, so a K tile's global loads are issued two MFMA
 // phases before the LDS write that consumes them (one phase in gemm_kernel: the HBM-missing A rows
 // of a new row band then stall that write, and through the barrier every wave of the block).  K
@@ -485,7 +418,7 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(Gemm
 template <int EPI, class C>
 __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel_d2(GemmArgs p) {
   constexpr int BM = C::BM, BN = C::BN, TM = C::TM, TN = C::TN, LROWS = C::LROWS, RA = C::RA, RB = C::RB;
-  __shared__ float lds[C::LDSA];
+  __shared__ float lds[C::LDSF];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv / C::WN, wn = wv % C::WN;
   const int nb = p.n / BN;
   const int K = p.k, ktiles = K / kKS;  // even (K % 64 == 0)
@@ -541,9 +474,6 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel_d2(G
   const int r = lane & 31, h = lane >> 5;
   f32x16 acc[TM][TN];
   auto mfma_tile = [&](int buf) {
-#if VSS_LT_PRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
     const float* As = lds + buf * (BM + BN) * kLS + (wm * C::WROWS + r) * kLS + h * 16;
     const float* Bs = lds + buf * (BM + BN) * kLS + BM * kLS + (wn * C::WCOLS + r) * kLS + h * 16;
 #pragma unroll
@@ -564,17 +494,8 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel_d2(G
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
           }
     }
-#if VSS_LT_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
   };
 
-#if VSS_LT_STAGGER
-  if (blockIdx.x >= gridDim.x / 2) {
-    const uint64_t t0 = wall_clock64();
-    while (wall_clock64() - t0 < (uint64_t)VSS_LT_STAGGER) __builtin_amdgcn_s_sleep(8);
-  }
-#endif
   float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 ra0[RA], rb0[RB], ra1[RA], rb1[RB];
   gload(ra0, rb0);  // K tile 0
@@ -606,21 +527,11 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel_d2(G
     }
     // epilogue through LDS buffer 1: every wave has passed the barrier after its last read of it,
     // and the next tile's first K tile sits in LDS 0
-#if VSS_LT_PROBE == 6  // profiling knob: no epilogue at all (accumulators kept live; timing only)
-    (void)row0; (void)col0;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) asm volatile("" ::"v"(acc[i][j][e]));
-#else
     // backward, exact shapes: no row masks (their branches made the compiler drain vmcnt to 0, i.e.
     // wait for the K tiles prefetched two ahead, at every y load; the forward measured ~1 % slower
     // without them, profiles/r02_gemm_epilogue_variants.log)
-    store_tile<EPI, TM, TN, !(VSS_LT_NOMASK && EPI == EPI_DTANH)>(p, acc, lds + (BM + BN) * kLS + wv * (32 * kES), row0 + wm * C::WROWS,
-                                            col0 + wn * C::WCOLS, csum);
-#endif
+    store_tile<EPI, TM, TN, EPI != EPI_DTANH>(p, acc, lds + (BM + BN) * kLS + wv * (32 * kES), row0 + wm * C::WROWS,
+                                              col0 + wn * C::WCOLS, csum);
     if (!has_next) break;
     __syncthreads();  // the next tile's second K tile is written into LDS 1 (the scratch)
     tile = next;
@@ -636,65 +547,37 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel_d2(G
 // summation order -- does not depend on the device the call runs on.
 constexpr int kGridCus = 256;
 
-#ifndef VSS_LT_CFG
-#define VSS_LT_CFG 256  // 256: 256 x 256 blocks for masked shapes with n % 256 == 0; 128: always 128 x 128
-#endif
-
-#ifndef VSS_LT_FWDCFG
-#define VSS_LT_FWDCFG 0  // profiling knob: forward exact shapes on 3 = 256 x 128 / 2 = 128 x 256 blocks (8 waves of 64 x 64)
-#endif
-#ifndef VSS_LT_BWDCFG
-#define VSS_LT_BWDCFG 0  // backward exact shapes: 0 = 128 x 128 blocks, 2 = 128 x 256, 3 = 256 x 128
-#endif
 
 // the launch plan of one GEMM: kernel, output tiles, grid
 struct Plan {
-  int kind;  // 0 Cfg128, 1 Cfg256, 2 Cfg128x256, 3 Cfg256x128
+  int kind;  // 0 Cfg128, 1 Cfg256
   int bn;
   int64_t tiles, grid;
 };
 
+// Exact shapes: rows % 128 == 0 and K % 32 == 0 (the update's layers but the first).
+static bool exact_shape(int64_t rows, int32_t k, int bm) { return rows % bm == 0 && k % kKS == 0; }
+
 static Plan plan(int64_t rows, int32_t k, int32_t n, bool forward) {
   Plan pl;
-  // Exact shapes (rows % 128 == 0, K % 32 == 0: the update's layers but the first) run the
-  // 128 x 128 blocks with unmasked, pipelined loads (fastest there); the masked form is fastest on
-  // 256 x 256 blocks (profiles/r01_gemm_fused_bench.log).
-  const bool exact = VSS_LT_EXACT && rows % Cfg128::BM == 0 && k % kKS == 0;
-  pl.kind = (VSS_LT_CFG == 256 && !exact && n % 256 == 0) ? 1 : 0;
+  // Exact shapes run the 128 x 128 blocks with unmasked, pipelined loads (fastest there); the masked
+  // form is fastest on 256 x 256 blocks (profiles/r01_gemm_fused_bench.log).
+  const bool exact = exact_shape(rows, k, Cfg128::BM);
+  pl.kind = (!exact && n % 256 == 0) ? 1 : 0;
   // the forward's exact shapes on 256 x 256 blocks with the two-deep pipeline: 123-134 TF vs 116-127 on
   // 128 x 128 (profiles/r02_gemm_d2c256.log); the backward's epilogue needs more registers than a
   // 256 x 256 block leaves (it spills), so it stays on 128 x 128
-  if (VSS_LT_D2CFG == 256 && VSS_LT_DEPTH == 2 && forward && exact && rows % Cfg256::BM == 0 && k % (2 * kKS) == 0 &&
-      n % 256 == 0)
-    pl.kind = 1;
-  if (VSS_LT_FWDCFG == 2 && VSS_LT_DEPTH == 2 && forward && exact && rows % Cfg128x256::BM == 0 && k % (2 * kKS) == 0 &&
-      n % Cfg128x256::BN == 0)
-    pl.kind = 2;
-  if (VSS_LT_FWDCFG == 3 && VSS_LT_DEPTH == 2 && forward && exact && rows % Cfg256x128::BM == 0 && k % (2 * kKS) == 0 &&
-      n % Cfg256x128::BN == 0)
-    pl.kind = 3;
-  if (VSS_LT_BWDCFG == 2 && VSS_LT_DEPTH == 2 && !forward && exact && rows % Cfg128x256::BM == 0 && k % (2 * kKS) == 0 &&
-      n % Cfg128x256::BN == 0)
-    pl.kind = 2;
-  if (VSS_LT_BWDCFG == 3 && VSS_LT_DEPTH == 2 && !forward && exact && rows % Cfg256x128::BM == 0 && k % (2 * kKS) == 0 &&
-      n % Cfg256x128::BN == 0)
-    pl.kind = 3;
-  static const int BMs[4] = {Cfg128::BM, Cfg256::BM, Cfg128x256::BM, Cfg256x128::BM};
-  static const int BNs[4] = {Cfg128::BN, Cfg256::BN, Cfg128x256::BN, Cfg256x128::BN};
-  static const int BPC[4] = {Cfg128::BLOCKS_PER_CU, Cfg256::BLOCKS_PER_CU, Cfg128x256::BLOCKS_PER_CU,
-                             Cfg256x128::BLOCKS_PER_CU};
-  const int bm = BMs[pl.kind];
-  pl.bn = BNs[pl.kind];
+  if (forward && exact && rows % Cfg256::BM == 0 && k % (2 * kKS) == 0 && n % 256 == 0) pl.kind = 1;
+  const int bm = pl.kind == 1 ? Cfg256::BM : Cfg128::BM;
+  const int bpc = pl.kind == 1 ? Cfg256::BLOCKS_PER_CU : Cfg128::BLOCKS_PER_CU;
+  pl.bn = pl.kind == 1 ? Cfg256::BN : Cfg128::BN;
   const int nb = n / pl.bn;
   pl.tiles = (rows + bm - 1) / bm * nb;
-  pl.grid = pl.tiles;
-#if VSS_LT_PERSIST
-  // min(tiles, blocks_per_cu x CUs), the latter rounded down to a multiple of 8 (XCD slots) and of
-  // nb (a fixed column tile per block)
-  int64_t g = (int64_t)kGridCus * BPC[pl.kind];
+  // persistent: min(tiles, blocks_per_cu x CUs), the latter rounded down to a multiple of 8 (XCD
+  // slots) and of nb (a fixed column tile per block)
+  int64_t g = (int64_t)kGridCus * bpc;
   g -= g % (8 * (int64_t)nb);
-  if (g > 0 && g < pl.tiles) pl.grid = g;
-#endif
+  pl.grid = (g > 0 && g < pl.tiles) ? g : pl.tiles;
   return pl;
 }
 
@@ -707,21 +590,11 @@ static bool shape_ok(int64_t rows, int32_t k, int32_t n) {
 template <int EPI, bool EXACT>
 static void launch_kind(const GemmArgs& a, const Plan& pl, hipStream_t s) {
   const dim3 grid((unsigned)pl.grid);
-  if constexpr (EXACT) {
-    if (pl.kind == 2) {
-      hipLaunchKernelGGL((gemm_kernel_d2<EPI, Cfg128x256>), grid, dim3(Cfg128x256::THREADS), 0, s, a);
-      return;
-    }
-    if (pl.kind == 3) {
-      hipLaunchKernelGGL((gemm_kernel_d2<EPI, Cfg256x128>), grid, dim3(Cfg256x128::THREADS), 0, s, a);
-      return;
-    }
-  }
-  if (VSS_LT_DEPTH == 2 && EXACT && pl.kind == 0 && a.k % (2 * kKS) == 0) {
+  if (EXACT && pl.kind == 0 && a.k % (2 * kKS) == 0) {
     hipLaunchKernelGGL((gemm_kernel_d2<EPI, Cfg128>), grid, dim3(Cfg128::THREADS), 0, s, a);
     return;
   }
-  if (VSS_LT_D2CFG == 256 && VSS_LT_DEPTH == 2 && EPI == EPI_TANH && EXACT && pl.kind == 1 && a.k % (2 * kKS) == 0) {
+  if (EPI == EPI_TANH && EXACT && pl.kind == 1 && a.k % (2 * kKS) == 0) {
     hipLaunchKernelGGL((gemm_kernel_d2<EPI_TANH, Cfg256>), grid, dim3(Cfg256::THREADS), 0, s, a);
     return;
   }
@@ -735,10 +608,7 @@ template <int EPI>
 static int launch(void* stream, const GemmArgs& a0, const Plan& pl) {
   GemmArgs a = a0;
   a.tiles = pl.tiles;
-  static const int BMs[4] = {Cfg128::BM, Cfg256::BM, Cfg128x256::BM, Cfg256x128::BM};
-  const int bm = BMs[pl.kind];
-  const bool exact = VSS_LT_EXACT && a.rows % bm == 0 && a.k % kKS == 0;
-  if (exact)
+  if (exact_shape(a.rows, a.k, pl.kind == 1 ? Cfg256::BM : Cfg128::BM))
     launch_kind<EPI, true>(a, pl, (hipStream_t)stream);
   else
     launch_kind<EPI, false>(a, pl, (hipStream_t)stream);
@@ -754,11 +624,8 @@ static int launch(void* stream, const GemmArgs& a0, const Plan& pl) {
 // with no barrier after the staging, one wave's tanh and stores run beside the other waves' MFMAs.
 // MFMA step (j, s): lane half h contributes k = 8j + 4h + s.
 constexpr int kFlThreads = 256;
-#ifndef VSS_LT_FIRST
-#define VSS_LT_FIRST 1  // profiling knob: 0 = the first layer on the tiled GEMM
-#endif
 
-static bool first_layer_ok(int32_t k, int32_t n) { return VSS_LT_FIRST && n == 256 && k % 4 == 0 && k > 48 && k <= 64; }
+static bool first_layer_ok(int32_t k, int32_t n) { return n == 256 && k % 4 == 0 && k > 48 && k <= 64; }
 
 template <int J>
 __global__ __launch_bounds__(kFlThreads, 2) void first_layer_kernel(int64_t rows, int k, const float* __restrict__ x,
@@ -837,12 +704,8 @@ struct SmallPlan {
   int64_t rows_per_block, blocks;
 };
 
-#ifndef VSS_LT_SMALLK
-#define VSS_LT_SMALLK 1  // profiling knob: 0 = the output layer's backward on the masked MFMA path
-#endif
-
 static bool small_k(int32_t k_next, int32_t n) {
-  return VSS_LT_SMALLK && (k_next == 4 || k_next == 8) && 1024 % n == 0;
+  return (k_next == 4 || k_next == 8) && 1024 % n == 0;
 }
 
 static SmallPlan small_plan(int64_t rows, int32_t n) {

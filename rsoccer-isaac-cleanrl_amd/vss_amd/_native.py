@@ -1,14 +1,16 @@
 """ctypes binding of libvss_amd.so — the C ABI declared in include/vss.h.
 
 The shared library is built in-tree by `make -C rsoccer-isaac-cleanrl_amd/csrc` (or
-`__graft_entry__.build()`).  There is no fallback: if the library is missing, or the device is
-not a ROCm GPU, the calls raise.  torch is imported first so that the HIP runtime the library
+`__graft_entry__.build()`).  There is no fallback: if the library is missing, was built from other
+sources than the tree's (its `vss_source_hash()` stamp differs from the hash of the sources here),
+or the device is not a ROCm GPU, the calls raise.  torch is imported first so that the HIP runtime the library
 links against (libamdhip64.so.7) is the one torch already loaded — one runtime, one set of
 streams.
 """
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 
 import torch  # noqa: F401  (loads torch's HIP runtime before the library resolves it)
@@ -18,12 +20,16 @@ LIB_PATH = os.path.join(HERE, "libvss_amd.so")
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "vss.h")
 
+# the sources the Makefile stamps into the library, in its order (csrc/Makefile STAMPED)
+STAMPED = (os.path.join(CSRC, "vss_step.hip"), os.path.join(CSRC, "vss_update.hip"),
+           os.path.join(CSRC, "vss_policy.hip"), HEADER, os.path.join(CSRC, "Makefile"))
+
 ABI_VERSION = 2
 MODE_FULL, MODE_SA, MODE_CMA, MODE_DMA = 0, 1, 2, 3
 STATE_CHANNELS = 58
 CH_BALL_X, CH_BALL_Y, CH_BALL_VX, CH_BALL_VY = 0, 1, 2, 3
 CH_RX, CH_RY, CH_RQX, CH_RQY, CH_RQZ, CH_RQW, CH_RVX, CH_RVY, CH_RW = 4, 10, 16, 22, 28, 34, 40, 46, 52
-EXPORTED = ("vss_abi_version", "vss_error_string", "vss_step", "vss_step_replay", "vss_rollout", "vss_reset_dones",
+EXPORTED = ("vss_abi_version", "vss_source_hash", "vss_error_string", "vss_step", "vss_step_replay", "vss_rollout", "vss_reset_dones",
             "vss_reset_dones_replay",
             "vss_compute_observations", "vss_mlp_packed_size", "vss_mlp_pack", "vss_policy_forward",
             "vss_value_forward_masked", "vss_episode_stats", "vss_tanh_grad_chunks", "vss_tanh_grad_bias",
@@ -71,8 +77,28 @@ class NativeError(RuntimeError):
 _lib = None
 
 
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) of the stamped sources as they are in this tree."""
+    h = hashlib.sha256()
+    for path in STAMPED:
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def verify_source_hash(lib: ctypes.CDLL, expected: str | None = None) -> None:
+    """Raise unless the library was built from the tree's sources (a stale prebuilt .so)."""
+    lib.vss_source_hash.restype = ctypes.c_char_p
+    built = lib.vss_source_hash().decode()
+    want = source_hash() if expected is None else expected
+    if built != want:
+        raise NativeError(
+            f"{LIB_PATH} was built from other sources (stamp {built}, tree {want}); rebuild it with "
+            f"`make -C {CSRC}` or `python -c 'import __graft_entry__ as g; g.build()'`")
+
+
 def load() -> ctypes.CDLL:
-    """Load libvss_amd.so (raises if it has not been built)."""
+    """Load libvss_amd.so (raises if it has not been built, or was built from other sources)."""
     global _lib
     if _lib is not None:
         return _lib
@@ -81,6 +107,7 @@ def load() -> ctypes.CDLL:
             f"VSS HIP library not found at {LIB_PATH}; build it with "
             f"`make -C {CSRC}` or `python -c 'import __graft_entry__ as g; g.build()'`")
     L = ctypes.CDLL(LIB_PATH)
+    verify_source_hash(L)
     P, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
     L.vss_abi_version.restype = ctypes.c_int
     L.vss_error_string.argtypes = [ctypes.c_int]

@@ -31,6 +31,29 @@ def test_library_loads_and_exports_every_declared_symbol():
     assert lib.vss_abi_version() == N.ABI_VERSION
 
 
+def test_library_is_built_from_the_tree_sources():
+    """The library's source stamp equals the hash of the sources in this tree, and a library whose
+    stamp differs (a stale prebuilt .so that travelled with the tree) is refused."""
+    lib = N.load()
+    N.verify_source_hash(lib)
+    with pytest.raises(N.NativeError, match="built from other sources"):
+        N.verify_source_hash(lib, expected="0" * 16)
+
+
+def test_stale_library_is_refused_at_load(tmp_path, monkeypatch):
+    """load() itself refuses a library whose stamp does not match the tree (here: the tree's
+    stamped sources replaced by a modified copy of one of them)."""
+    import shutil
+    src = os.path.join(tmp_path, "vss_step.hip")
+    shutil.copy(N.STAMPED[0], src)
+    with open(src, "a") as f:
+        f.write("// edited after the build\n")
+    monkeypatch.setattr(N, "STAMPED", (src,) + tuple(N.STAMPED[1:]))
+    monkeypatch.setattr(N, "_lib", None)
+    with pytest.raises(N.NativeError, match="built from other sources"):
+        N.load()
+
+
 def test_error_strings():
     lib = N.load()
     assert lib.vss_error_string(0) == b"ok"

@@ -24,7 +24,7 @@ run() {  # run <name> <seconds> <cmd...>
 }
 
 STEPS=${STEPS:-tests,smoke,bench,prof}
-case ",$STEPS," in *,tests,*) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;; esac
+case ",$STEPS," in *,tests,*) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;; esac
 case ",$STEPS," in *,tplay,*) run pytest_play 600 python -m pytest tests/test_play.py -m gpu -x -q ;; esac
 case ",$STEPS," in *,smoke,*) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;; esac
 case ",$STEPS," in *,bench,*) run bench 400 python bench.py; run bench_eager 300 python bench.py --graph 0 --no-cpu-baseline ;; esac
@@ -46,10 +46,6 @@ case ",$STEPS," in *,pmcl3,*)
   run rocprof_write_l3 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_l3_$TAG" -o run -- \
       python3 bench.py --fields 131072 --steps 20 --warmup 5 --no-cpu-baseline --ppo-updates 0 --l3-check-fields 0 --rollout-k 0 ;;
 esac
- case ",$STEPS," in *,ablate,*) run ablate 300 python tools/ablate.py ;; esac
-case ",$STEPS," in *,ablsa,*)
-  ABLATE_MODE=sa ABLATE_REPS=7 run ablate_sa 300 python tools/ablate.py
-  ABLATE_MODE=full ABLATE_REPS=7 run ablate_full 300 python tools/ablate.py ;; esac
 case ",$STEPS," in *,tupd,*) run pytest_update 600 python -m pytest tests/test_update.py tests/test_ppo.py -m gpu -x -q ;; esac
 # the update's fused-epilogue GEMMs: unit tests, kernel bench vs torch, PPO update fused vs split
 case ",$STEPS," in *,gemm,*)

@@ -187,11 +187,13 @@ def past_l3_leg(n: int, steps: int, dev) -> dict:
         N.check(lib.vss_step(stream, n, N.MODE_FULL, byref(prm), byref(st), byref(cios[k % 4])), "vss_step")
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    rc = 0
     e0.record()
     for k in range(steps):
-        lib.vss_step(stream, n, N.MODE_FULL, byref(prm), byref(st), byref(cios[k % 4]))
+        rc |= lib.vss_step(stream, n, N.MODE_FULL, byref(prm), byref(st), byref(cios[k % 4]))
     e1.record()
     torch.cuda.synchronize()
+    N.check(rc, "vss_step (past_l3 timed launches)")  # a failed launch must not report a rate
     ms = e0.elapsed_time(e1) / steps
     algo = BYTES["full"] * n
     del env

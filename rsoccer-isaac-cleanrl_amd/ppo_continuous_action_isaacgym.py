@@ -372,6 +372,34 @@ def first_done_stats(done: torch.Tensor, info: dict) -> torch.Tensor:
     return torch.stack([d.max()] + [info["r"][k][idx].float() for k in EP_KEYS] + [info["l"][idx].float()])
 
 
+class TerminalValues:
+    """next_values[t] = critic(terminal_obs_t) (ppo…:272) for the fused rollout, in ONE masked critic
+    pass after the rollout instead of a critic pass per step.  For a field that did not reset at
+    step t the terminal observation IS next_obs_t, whose value the next step computes (values[t+1],
+    or critic(next_obs) after the last step), so only the reset rows need the terminal pass; the
+    critic does not change within a rollout, so one pass over all T x E recorded terminal
+    observations, masked by the dones, gives the same values.  (A masked pass per step cost
+    ~0.22 ms however few rows reset -- one wave's serial walk through the critic.)  Memory: the
+    (T, E, obs) fp32 copy of the terminal observations, 1.7 GB at T = 128, E = 65,536 and 5.1 GB
+    for DMA at 196,608 agent rows (<= 2 % of one MI355X's 288 GB)."""
+
+    def __init__(self, T, E, obs_shape, device):
+        self.T, self.E = T, E
+        self.term_obs = torch.zeros((T, E) + tuple(obs_shape), device=device)
+        self.term_mask = torch.zeros((T, E), device=device, dtype=torch.long)
+        self.term_values = torch.zeros((T, E), device=device)
+
+    def record(self, step, terminal_obs, done):
+        self.term_obs[step].copy_(terminal_obs.reshape(self.term_obs.shape[1:]))
+        self.term_mask[step].copy_(done)
+
+    def next_values(self, fused, values, next_dones, next_obs):
+        """(T, E) next_values: the masked terminal pass where a field reset, else values[t + 1]."""
+        fused.get_value_masked(self.term_obs, self.term_mask, self.term_values.view(self.T * self.E, 1))
+        v_last = fused.get_value(next_obs).view(1, self.E)
+        return torch.where(next_dones.bool(), self.term_values, torch.cat([values[1:], v_last], 0))
+
+
 def compute_gae(rewards, values, next_values, next_dones, next_timeouts, gamma, lam):
     """Timeout-aware GAE of ppo…:282-296 (terminal-obs bootstrap, reversed scan over T)."""
     T = rewards.shape[0]
@@ -408,6 +436,32 @@ def normalize_advantages(mb_adv: torch.Tensor, world: int = 1, global_stats: boo
     return (mb_adv - mean.float()) / (std.float() + 1e-8)
 
 
+def annealed_lr(update: int, num_updates: int, lr0: float) -> float:
+    """--anneal-lr (ppo…:251-253): linear decay from lr0 at update 1 to lr0 / num_updates at the last."""
+    frac = 1.0 - (update - 1.0) / num_updates
+    return frac * lr0
+
+
+def adapted_lr(lr: float, approx_kl: float, threshold_kl: float) -> float:
+    """--adaptative-lr (ppo…:356-361), after every minibatch: /1.5 (floor 1e-6) when the KL estimate
+    exceeds 2 x threshold, x1.5 (cap 1e-2) when it is below threshold / 2, else unchanged."""
+    if approx_kl > 2.0 * threshold_kl:
+        return max(lr / 1.5, 1e-6)
+    if approx_kl < 0.5 * threshold_kl:
+        return min(lr * 1.5, 1e-2)
+    return lr
+
+
+def value_loss(newvalue, mb_returns, mb_values, clip_coef: float, clip_vloss: bool):
+    """The value loss of ppo…:335-346: 0.5 mean (v - R)^2, or with --clip-vloss the elementwise max
+    of that and the loss of v clipped to within clip_coef of the rollout's value."""
+    if clip_vloss:
+        v_unclipped = (newvalue - mb_returns) ** 2
+        v_clipped = mb_values + torch.clamp(newvalue - mb_values, -clip_coef, clip_coef)
+        return 0.5 * torch.max(v_unclipped, (v_clipped - mb_returns) ** 2).mean()
+    return 0.5 * ((newvalue - mb_returns) ** 2).mean()
+
+
 def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_advantages, b_returns,
                b_values, world=1, gen=None):
     """Clipped PPO over update_epochs x num_minibatches (ppo…:306-365).  Returns last-minibatch
@@ -417,7 +471,9 @@ def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_adv
     mb = batch // args.num_minibatches
     clipfracs = []
     stats = {}
+    epochs_run = 0
     for epoch in range(args.update_epochs):
+        epochs_run += 1
         b_inds = torch.randperm(batch, device=device, generator=gen)
         for start in range(0, batch, mb):
             mb_inds = b_inds[start:start + mb]
@@ -437,13 +493,7 @@ def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_adv
             if args.norm_adv:
                 mb_adv = normalize_advantages(mb_adv, world, getattr(args, "global_adv_norm", True))
             pg_loss = torch.max(-mb_adv * ratio, -mb_adv * torch.clamp(ratio, 1 - args.clip_coef, 1 + args.clip_coef)).mean()
-            newvalue = newvalue.view(-1)
-            if args.clip_vloss:
-                v_unclipped = (newvalue - b_returns[mb_inds]) ** 2
-                v_clipped = b_values[mb_inds] + torch.clamp(newvalue - b_values[mb_inds], -args.clip_coef, args.clip_coef)
-                v_loss = 0.5 * torch.max(v_unclipped, (v_clipped - b_returns[mb_inds]) ** 2).mean()
-            else:
-                v_loss = 0.5 * ((newvalue - b_returns[mb_inds]) ** 2).mean()
+            v_loss = value_loss(newvalue.view(-1), b_returns[mb_inds], b_values[mb_inds], args.clip_coef, args.clip_vloss)
             entropy_loss = entropy.mean()
             loss = pg_loss - args.ent_coef * entropy_loss + v_loss * args.vf_coef
 
@@ -458,17 +508,13 @@ def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_adv
                     dist.all_reduce(approx_kl, op=dist.ReduceOp.SUM)
                     approx_kl /= world
             if args.adaptative_lr:
-                lr = optimizer.param_groups[0]["lr"]
-                kl = float(approx_kl)
-                if kl > 2.0 * args.threshold_kl:
-                    optimizer.param_groups[0]["lr"] = max(lr / 1.5, 1e-6)
-                elif kl < 0.5 * args.threshold_kl:
-                    optimizer.param_groups[0]["lr"] = min(lr * 1.5, 1e-2)
+                optimizer.param_groups[0]["lr"] = adapted_lr(optimizer.param_groups[0]["lr"], float(approx_kl),
+                                                             args.threshold_kl)
         if args.target_kl is not None and float(approx_kl) > args.target_kl:
             break
     stats.update(v_loss=v_loss.detach(), pg_loss=pg_loss.detach(), entropy=entropy_loss.detach(),
                  old_approx_kl=old_approx_kl, approx_kl=approx_kl,
-                 clipfrac=torch.stack(clipfracs).mean())
+                 clipfrac=torch.stack(clipfracs).mean(), epochs_run=epochs_run)
     return stats
 
 
@@ -574,13 +620,7 @@ def train(args):
     next_timeouts = torch.zeros((T, E), device=device)
     values = torch.zeros((T, E), device=device)
     next_values = torch.zeros((T, E), device=device)
-    term_values = torch.zeros((T, E), device=device)  # fused path: critic(terminal obs) of reset fields
-    if fused is not None:
-        # the rollout's terminal observations and dones, for ONE masked critic pass after the rollout
-        # (the critic does not change during it): a masked pass per step cost ~0.22 ms however few
-        # rows reset -- one wave's serial walk through the critic -- against a 14 MB copy per step
-        term_obs = torch.zeros((T, E) + obs_dim, device=device)
-        term_mask = torch.zeros((T, E), device=device, dtype=torch.long)
+    term = TerminalValues(T, E, obs_dim, device) if fused is not None else None
 
     global_step = 0
     start_time = time.time()
@@ -589,7 +629,7 @@ def train(args):
     history = []
     for update in range(1, num_updates + 1):
         if args.anneal_lr:
-            optimizer.param_groups[0]["lr"] = (1.0 - (update - 1.0) / num_updates) * args.learning_rate
+            optimizer.param_groups[0]["lr"] = annealed_lr(update, num_updates, args.learning_rate)
         t_roll = time.time()
         ep_ret = torch.zeros((), device=device)
         ep_cnt = torch.zeros((), device=device)
@@ -613,11 +653,8 @@ def train(args):
             next_obs, rewards[step], next_done, info = envs.step(action)
             next_dones[step] = next_done
             next_timeouts[step] = info["time_outs"]
-            if fused is not None:
-                # critic(terminal obs) only where the field reset (ppo…:272), after the rollout:
-                # elsewhere the terminal observation IS next_obs, whose value the next step computes
-                term_obs[step].copy_(info["terminal_observation"].reshape((E,) + obs_dim))
-                term_mask[step].copy_(next_done)
+            if term is not None:  # critic(terminal obs) after the rollout (TerminalValues)
+                term.record(step, info["terminal_observation"], next_done)
             else:
                 with torch.no_grad(), autocast(args, device):
                     next_values[step] = agent.get_value(info["terminal_observation"]).reshape(1, -1)
@@ -626,11 +663,8 @@ def train(args):
             ep_cnt += d.sum()
             if step <= 2:
                 ep_first[step] = first_done_stats(d, info)
-        if fused is not None:
-            fused.get_value_masked(term_obs, term_mask, term_values.view(T * E, 1))
-            v_last = fused.get_value(next_obs).view(1, E)
-            nxt = torch.cat([values[1:], v_last], 0)
-            next_values = torch.where(next_dones.bool(), term_values, nxt)
+        if term is not None:
+            next_values = term.next_values(fused, values, next_dones, next_obs)
         if device.type == "cuda":
             torch.cuda.synchronize()
         t_roll = time.time() - t_roll

@@ -19,7 +19,7 @@ absent, so the dynamics are the build's own model; everything else (pre/post phy
 rewards, dones, obs, reset sampling, OU wrappers, time-outs) is the reference's own code.
 All torch.rand / torch.normal draws are recorded so the oracle can replay them.
 
-Usage:  python tests/golden/gen_golden.py   (writes tests/golden/*.npz)
+Usage:  python tests/golden/gen_golden.py [g1 g4 g5 g6]   (writes tests/golden/*.npz; default all)
 """
 from __future__ import annotations
 
@@ -536,7 +536,13 @@ def gen_full_rollout(rec: Recorder, n=16, steps=1000, max_len=400):
 
 
 def gen_wrapped(rec: Recorder, mode: str, n=6, steps=60, max_len=25):
-    """G5: SingleAgent / CMA / DMA wrappers (envs/wrappers.py:89-180) on the reference VSS."""
+    """G5: SingleAgent / CMA / DMA wrappers (envs/wrappers.py:89-180) on the reference VSS.
+    Goals are forced (play.py-style external writes through the reference's views, as in G4) at
+    both ends of the field and at several points of an episode: blue and yellow scoring at the
+    first step and mid-episode, and into fields still in their first episode at steps max_len - 3
+    (a goal done with time_outs = 0) and max_len - 2 (the time-out edge: time_outs = 1), so the
+    wrapped path's goal channel, mid-episode OU-buffer zeroing and time_outs on a goal done are
+    all pinned (envs/wrappers.py:101-115, 133-148, 163-180; envs/vss.py:578-594)."""
     from envs.wrappers import SingleAgent, CMA, DMA
     torch.manual_seed(3)
     rec.take()
@@ -552,8 +558,23 @@ def gen_wrapped(rec: Recorder, mode: str, n=6, steps=60, max_len=25):
     keep = {k: [] for k in ("actions", "obs", "terminal_obs", "reward", "rews", "dones", "time_outs",
                             "progress_f", "state", "action_buf", "n_u", "n_z")}
     U, Z, S, NC = [], [], [], []
+    forced_steps, forced_state = [], []
+    edge = {max_len - 3: None, max_len - 2: None}
+    schedule = {0: [(3, -1.0)], 7: [(0, 1.0), (1, -1.0)], 40: [(4, -1.0), (5, 1.0)]}
     for t in range(steps):
         a = gen.uniform(-1.2, 1.2, (rows, adim)).astype(np.float32)
+        push = list(schedule.get(t, []))
+        if t in edge:  # a field still in its first episode (progress == t before this step)
+            cand = [f for f in range(n) if int(env.progress_buf[f]) == t and f not in edge.values()]
+            assert cand, f"no first-episode field left at step {t}"
+            edge[t] = cand[0]
+            push.append((cand[0], 1.0 if t % 2 else -1.0))
+        if push:
+            for f, side in push:
+                env.ball_pos[f] = torch.tensor([0.74 * side, 0.05]); env.ball_vel[f] = torch.tensor([1.0 * side, 0.0])
+            env.gym.set_actor_root_state_tensor(env.sim, env.root_state)
+            forced_steps.append(t)
+            forced_state.append(root_to_state(env.root_state.reshape(-1, 13), n)[LIVE])
         obs, reward, dones, info = W.step(torch.from_numpy(a))
         u, z = rec.take()
         sz = rec.take_sizes()
@@ -574,8 +595,12 @@ def gen_wrapped(rec: Recorder, mode: str, n=6, steps=60, max_len=25):
                         u_sizes=np.concatenate(S), u_ncalls=np.array(NC),
                         init_state=init_state, uniforms=np.concatenate(U), normals=np.concatenate(Z),
                         live_channels=np.array(LIVE), max_len=np.array(max_len), num_envs=np.array(W.num_envs),
+                        forced_steps=np.array(forced_steps), forced_state=np.stack(forced_state),
+                        edge_steps=np.array(sorted(edge)), edge_fields=np.array([edge[k] for k in sorted(edge)]),
                         **out)
-    print(f"G5 {mode}: rows {rows} steps {steps} dones {int(out['dones'].sum())} num_envs {W.num_envs}")
+    goal = np.abs(out["rews"][..., 0]) > 0
+    print(f"G5 {mode}: rows {rows} steps {steps} dones {int(out['dones'].sum())} goal rows {int(goal.sum())} "
+          f"goal dones with time_outs=0 {int((goal & (out['time_outs'] == 0)).sum())} num_envs {W.num_envs}")
 
 
 def gen_agent():
@@ -607,17 +632,21 @@ def gen_agent():
     print("G6: agent params", int(res["a2_nparams"]), int(res["a6_nparams"]))
 
 
-def main():
+def main(which=("g1", "g4", "g5", "g6")):
     install_stubs()
     O.build()
     rec = Recorder()
     rec.install()
-    gen_obs_and_rewards(rec)
-    gen_full_rollout(rec)
-    for mode in ("sa", "cma", "dma"):
-        gen_wrapped(rec, mode)
-    gen_agent()
+    if "g1" in which:
+        gen_obs_and_rewards(rec)
+    if "g4" in which:
+        gen_full_rollout(rec)
+    if "g5" in which:
+        for mode in ("sa", "cma", "dma"):
+            gen_wrapped(rec, mode)
+    if "g6" in which:
+        gen_agent()
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]) or ("g1", "g4", "g5", "g6"))

@@ -23,6 +23,7 @@ import numpy as np
 
 SCALE = np.array([np.float32(1.5) - np.float32(0.14), np.float32(1.3) - np.float32(0.14)], np.float32)  # envs/vss.py:142-147
 MIN_DIST = np.float32(0.07)  # min_robot_placement_dist, envs/vss.py:48-49
+MAX_ROUNDS = 64  # the kernels' rejection bound (csrc/vss_step.hip kMaxRejectRounds)
 PAIRS = [(i, j) for i in range(7) for j in range(i + 1, 7)]  # entities_pairs (all 21)
 
 
@@ -63,6 +64,7 @@ def to_rows(flat: np.ndarray, env_ids, n_fields: int, call_sizes=None):
     assert pos == len(flat), f"consumed {pos} of {len(flat)} reference draws"
     if call_sizes is not None:
         assert list(sizes) == [int(c) for c in call_sizes], f"round sizes {sizes} != reference calls {list(call_sizes)}"
+    assert rounds.max(initial=0) <= MAX_ROUNDS, "more rejection rounds than the kernels bound (vss_step.hip kMaxRejectRounds)"
     stride = 14 * max(1, int(rounds.max(initial=0))) + 8
     rows = np.zeros((n_fields, stride), np.float32)
     for i, f in enumerate(ids):

@@ -8,7 +8,8 @@ by step, exactly like tests/test_oracle_golden.py checks the oracle:
 
   * G4 = BASELINE config 1: 16 fields x 1,000 steps of the raw VSS.step (FULL contract), with
     goals forced at the time-out edge;
-  * G5: SingleAgent / CMA / DMA wrappers, 6 fields x 60 steps;
+  * G5: SingleAgent / CMA / DMA wrappers, 6 fields x 60 steps, with goals forced at both ends,
+    mid-episode and at the time-out edge;
   * the construction-time reset (VSS.__init__ -> reset_dones over every field).
 
 Bar: integers (progress, reset, dones, time-outs) bit-exact; floats bit-exact except values that
@@ -23,7 +24,7 @@ import torch
 
 import oracle as O
 import replay_draws as RD
-from test_oracle_golden import TRIG_ATOL, assert_obs_equal, load
+from test_oracle_golden import TRIG_ATOL, assert_obs_equal, assert_wrapped_goals_pinned, load
 from vss_amd import _native as N
 
 pytestmark = pytest.mark.gpu
@@ -180,13 +181,16 @@ def test_wrapped_step_replay_matches_reference(golden_dir, mode_name):
     ml = int(g["max_len"])
     draws = step_draws(g, g["dones"][:, ::R])
     normals = RD.split_steps(g["normals"], g["n_z"])
+    forced = {int(t): i for i, t in enumerate(g["forced_steps"])}
     dev = DevEnv(n, mode)
     for t in range(T):
         if t == 0:
-            dev.set_live(live, g["init_state"][live], np.zeros(n), np.ones(n), np.zeros((n, 12)))
+            pre = g["forced_state"][forced[0]] if 0 in forced else g["init_state"][live]
+            dev.set_live(live, pre, np.zeros(n), np.ones(n), np.zeros((n, 12)))
             ou = np.zeros((n, 12), np.float32)
         else:
-            dev.set_live(live, g["state"][t - 1], g["progress_f"][t - 1][::R].astype(np.int64), g["dones"][t - 1][::R])
+            pre = g["forced_state"][forced[t]] if t in forced else g["state"][t - 1]
+            dev.set_live(live, pre, g["progress_f"][t - 1][::R].astype(np.int64), g["dones"][t - 1][::R])
             ou = g["action_buf"][t - 1]
         dev.io["ou_buf"].copy_(torch.from_numpy(np.ascontiguousarray(ou, np.float32)))
         assert normals[t].size == 12 * n, "random_ou draws one (N, 2, 3, 2) normal tensor per step"
@@ -204,7 +208,7 @@ def test_wrapped_step_replay_matches_reference(golden_dir, mode_name):
         assert_obs_equal(dev.host("obs"), g["obs"][t], agents=agents)
         assert_obs_equal(dev.host("terminal_obs"), g["terminal_obs"][t], agents=agents)
         assert_state(dev, live, g["state"][t], msg)
-    assert g["dones"].sum() > 0
+    assert_wrapped_goals_pinned(g, R)
 
 
 def test_replay_entries_reject_bad_draws():
@@ -224,3 +228,7 @@ def test_replay_entries_reject_bad_draws():
     assert L.vss_step_replay(s, 4, O.MODE_SA, ctypes.byref(prm), ctypes.byref(st), ctypes.byref(io), ctypes.byref(no_normals)) == 1
     assert L.vss_step_replay(s, 4, O.MODE_SA, ctypes.byref(prm), ctypes.byref(st), ctypes.byref(io), None) == 1
     assert L.vss_reset_dones_replay(s, 4, ctypes.byref(prm), ctypes.byref(st), ctypes.byref(short)) == 1
+    # a row holding more rejection rounds than the kernel's bound (64) is refused, not replayed short
+    too_many = N.VssReplayDraws(u.data_ptr(), 14 * 65 + 8, u.data_ptr())
+    assert L.vss_step_replay(s, 4, O.MODE_SA, ctypes.byref(prm), ctypes.byref(st), ctypes.byref(io), ctypes.byref(too_many)) == 1
+    assert L.vss_reset_dones_replay(s, 4, ctypes.byref(prm), ctypes.byref(st), ctypes.byref(too_many)) == 1

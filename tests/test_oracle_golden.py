@@ -174,16 +174,15 @@ def test_wrapped_step_matches_reference(golden_dir, mode_name):
     quat = np.isin(live, list(range(O.CH_RQZ, O.CH_RQZ + 12)))
     u_off = np.concatenate([[0], np.cumsum(g["n_u"])])
     z_off = np.concatenate([[0], np.cumsum(g["n_z"])])
+    forced = {int(t): i for i, t in enumerate(g["forced_steps"])}
     for t in range(T):
         if t == 0:
-            env = O.HostEnv(n)
-            env.state[:] = g["init_state"]
-            env.progress[:] = 0
-            env.reset[:] = 1
+            pre = g["forced_state"][forced[0]] if 0 in forced else g["init_state"][live]
+            env = _env_from_live(n, live, pre, np.zeros(n, np.int64), np.ones(n, np.int64))
             ou = np.zeros((n, 12), np.float32)
         else:
-            env = _env_from_live(n, live, g["state"][t - 1], g["progress_f"][t - 1][::R].astype(np.int64),
-                                 g["dones"][t - 1][::R])
+            pre = g["forced_state"][forced[t]] if t in forced else g["state"][t - 1]
+            env = _env_from_live(n, live, pre, g["progress_f"][t - 1][::R].astype(np.int64), g["dones"][t - 1][::R])
             ou = g["action_buf"][t - 1].copy()
         io = O.make_io(n, mode)
         io["ou_buf"][:] = ou
@@ -204,9 +203,29 @@ def test_wrapped_step_matches_reference(golden_dir, mode_name):
         st = env.state[live]
         np.testing.assert_array_equal(st[~quat], g["state"][t][~quat])
         np.testing.assert_allclose(st[quat], g["state"][t][quat], atol=TRIG_ATOL, rtol=0)
-    assert g["dones"].sum() > 0
+    assert_wrapped_goals_pinned(g, R)
     if mode == O.MODE_DMA:
         assert int(g["num_envs"]) == 3 * n  # DMA re-assigns num_environments (envs/wrappers.py:154)
+
+
+def assert_wrapped_goals_pinned(g, R):
+    """A G5 fixture exercises goal terminations (not only time-outs): goal-channel rewards of both
+    signs, goal dones with time_outs = 0 (mid-episode: the OU buffer is zeroed mid-episode), and a
+    goal at progress max_len - 1, where the reference's formula makes it a time-out
+    (envs/vss.py:578-594, 634-655; Ext VecTask.step)."""
+    goal = g["rews"][..., 0]
+    done = g["dones"] != 0
+    assert (goal > 0).sum() > 0 and (goal < 0).sum() > 0, "both teams must score"
+    assert ((goal != 0) & done & (g["time_outs"] == 0)).sum() >= 4 * R, "goal dones with time_outs = 0"
+    assert ((goal == 0) & done & (g["time_outs"] == 1)).sum() > 0, "plain time-outs"
+    ml = int(g["max_len"])
+    (t2, t1), (f2, f1) = g["edge_steps"], g["edge_fields"]
+    assert (t2, t1) == (ml - 3, ml - 2)
+    assert g["progress_f"][t1, f1 * R] == ml - 1 and g["time_outs"][t1, f1 * R] == 1 and goal[t1, f1 * R] != 0
+    assert g["progress_f"][t2, f2 * R] == ml - 2 and g["time_outs"][t2, f2 * R] == 0 and goal[t2, f2 * R] != 0
+    # a goal done mid-episode zeroes the done field's OU action buffer (envs/wrappers.py:105-107)
+    mid = np.nonzero((goal[:, ::R] != 0) & (g["time_outs"][:, ::R] == 0))
+    assert len(mid[0]) > 0 and np.all(g["action_buf"][mid[0], mid[1]] == 0)
 
 
 def test_reset_placement_threshold_is_exact():

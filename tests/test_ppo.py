@@ -210,10 +210,13 @@ def test_train_sa_65536_envs_config3(tmp_path):
 
 
 @pytest.mark.gpu
-def test_fused_rollout_next_values_equal_reference_definition(tmp_path):
+@pytest.mark.parametrize("form", ["per_step", "batched"])
+def test_fused_rollout_next_values_equal_reference_definition(tmp_path, form):
     """With the fused policy the PPO loop reconstructs next_values[t] = critic(terminal_obs_t)
     (ppo…:272) from values[t+1] and the masked terminal pass.  Check the identity directly: run a
-    short SA rollout and compare with critic(terminal_obs) evaluated for every row."""
+    short SA rollout and compare with critic(terminal_obs) evaluated for every row -- with the
+    masked pass once per step ("per_step") and in the form train() uses ("batched":
+    TerminalValues records every step, then ONE masked pass over all T x E rows)."""
     from envs.vss import default_cfg
     from envs.wrappers import SingleAgent
     from envs.vss import VSS
@@ -230,17 +233,24 @@ def test_fused_rollout_next_values_equal_reference_definition(tmp_path):
     term = torch.zeros((T, E), device="cuda")
     full = torch.zeros((T, E), device="cuda")
     dones = torch.zeros((T, E), device="cuda")
+    tv = P.TerminalValues(T, E, (52,), "cuda")
     o = W.reset()["obs"]
     for t in range(T):
         a, lp, _, v = fused.get_action_and_value(o)
         values[t] = v.flatten()
         ob, r, d, info = W.step(a)
         dones[t] = d
-        fused.get_value_masked(info["terminal_observation"], d, term[t].view(E, 1))
+        if form == "per_step":
+            fused.get_value_masked(info["terminal_observation"], d, term[t].view(E, 1))
+        else:
+            tv.record(t, info["terminal_observation"], d)
         full[t] = fused.get_value(info["terminal_observation"]).flatten()
         o = ob["obs"]
-    v_last = fused.get_value(o).view(1, E)
-    nv = torch.where(dones.bool(), term, torch.cat([values[1:], v_last], 0))
+    if form == "per_step":
+        v_last = fused.get_value(o).view(1, E)
+        nv = torch.where(dones.bool(), term, torch.cat([values[1:], v_last], 0))
+    else:
+        nv = tv.next_values(fused, values, dones, o)
     assert dones.sum() > 0
     assert torch.equal(nv, full)
 

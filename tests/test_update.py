@@ -214,17 +214,20 @@ def test_fused_gemm_refusals_gpu():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("act_dim", [2, 6])
 @pytest.mark.parametrize("mlp", ["fused", "split"])
 @pytest.mark.parametrize("rows", [256, 65536 + 64 * 3])
-def test_update_gradients_through_hip_match_autograd_gpu(rows, mlp, monkeypatch):
+def test_update_gradients_through_hip_match_autograd_gpu(rows, mlp, act_dim, monkeypatch):
     """The update's forward equals the Agent's (bit for bit on the hipBLASLt path "split"; within
     fp32 GEMM rounding on the fused-GEMM path); its gradients (fused HIP GEMM epilogues or the HIP
-    tanh backward + bias, split-K dW) equal autograd's up to fp32 summation order."""
+    tanh backward + bias, split-K dW) equal autograd's up to fp32 summation order.  act_dim 6 (the
+    CMA actor: 6 output columns padded to k_pad = 8 in vss_output_backward) as well as 2 (SA/DMA:
+    k_pad = 4; the 1-column critic pads to 4 in both)."""
     monkeypatch.setattr(P, "UPDATE_MLP", mlp)
-    agent = make_agent(2).cuda()
+    agent = make_agent(act_dim).cuda()
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.randn(rows, 52, device="cuda", generator=g)
-    a = torch.randn(rows, 2, device="cuda", generator=g) * 0.5
+    a = torch.randn(rows, act_dim, device="cuda", generator=g) * 0.5
     outs_ref = agent.get_action_and_value(x, a)
     loss_ref = outs_ref[1].sum() + outs_ref[2].sum() + outs_ref[3].sum()
     grads_ref = torch.autograd.grad(loss_ref, list(agent.parameters()))

@@ -142,11 +142,17 @@ __device__ __forceinline__ void mfma_layer(const float* __restrict__ wp, const f
 #pragma unroll
     for (int nt = 0; nt < NTP; ++nt) acc[nt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     f32x4 stage[PER_LANE];
-    // chunk 0 -> buffer 0
+    // chunk 0 -> buffer 0: every load issued before the first LDS write (one wait, not one per load)
 #pragma unroll
     for (int j = 0; j < PER_LANE; ++j) {
       const int e = wave * PER_WAVE + j * 64 + lane;
-      if (e < (wave + 1) * PER_WAVE && e < CH_F4 && in_layer(0, e)) l4[e] = g4[gidx(p, 0, e)];
+      if (e < (wave + 1) * PER_WAVE && e < CH_F4 && in_layer(0, e)) stage[j] = g4[gidx(p, 0, e)];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < PER_LANE; ++j) {
+      const int e = wave * PER_WAVE + j * 64 + lane;
+      if (e < (wave + 1) * PER_WAVE && e < CH_F4 && in_layer(0, e)) l4[e] = stage[j];
     }
     __syncthreads();
 #pragma unroll
@@ -160,6 +166,7 @@ __device__ __forceinline__ void mfma_layer(const float* __restrict__ wp, const f
           if (e < (wave + 1) * PER_WAVE && e < CH_F4 && in_layer(c + 1, e)) stage[j] = g4[gidx(p, c + 1, e)];
         }
       }
+      __builtin_amdgcn_sched_barrier(0);  // the next chunk's loads stay ahead of this chunk's MFMAs
       const f32x4* cur = l4 + buf * (kChunkFloats / 4);
       // the weights of k-step u + 1 are read from LDS while k-step u's MFMAs run (two register
       // sets), so the LDS latency hides behind NQP x 4 MFMAs instead of stalling every group

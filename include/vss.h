@@ -274,6 +274,17 @@ int vss_linear_tanh(void* stream, int64_t rows, int32_t k_in, int32_t n_out, con
                     const float* bias, float* y);
 
 /*
+ * vss_linear_tanh for the LAST hidden layer with the output layer folded in (ppo…:104-111: Linear(512,
+ * 256), Tanh, Linear(256, k_out)): y = tanh(x W^T + b) as vss_linear_tanh, and
+ *   out_part[s][r][a] = sum over the 64 columns c of slice s (s = 0..3) of y[r][c] w_out[a][c]
+ * so the output layer is out = sum_s out_part[s] + b_out without a second read of y.  n_out = 256,
+ * rows % 256 == 0, k_in % 64 == 0, k_out in {1, 2, 6}; w_out (k_out, 256) row-major; out_part
+ * (4, rows, k_out).  VSS_E_ARG for other shapes (the caller uses vss_linear_tanh + a GEMM then).
+ */
+int vss_linear_tanh_out(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
+                        const float* bias, float* y, int32_t k_out, const float* w_out, float* out_part);
+
+/*
  * The backward through a layer and the tanh below it (autograd of nn.Linear → nn.Tanh,
  * ppo…:104-111, in loss.backward() at ppo…:357) in one launch on the fp32 matrix cores:
  *   grad_in = (grad_next W_next) * (1 - y^2),   bias_partial[c][j] = sum of grad_in[r][j] over part c

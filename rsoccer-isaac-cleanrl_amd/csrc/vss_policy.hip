@@ -11,44 +11,71 @@
 // so an MFMA accumulator holds 4 output features of one sample per lane (lane l: sample l&15,
 // features 16*tile + 4*(l>>4) + r) — exactly the B-operand a following 16x16x4 MFMA needs when
 // its k-step (t, r) takes input feature 16t + 4*(l>>4) + r.  Activations therefore stay in
-// registers from the first layer to the last (no LDS, no HBM round trips).  The weights are
-// repacked once per update (vss_mlp_pack) into that k order and lane order, so each MFMA's A
-// operand is one coalesced float4 load (4 output tiles) from L2.  Bias + tanh, the tiny output
-// layer (VALU dot products + cross-lane reduction), Gaussian sampling (Philox), log-prob and
+// registers from the first layer to the last (no LDS, no HBM round trips).  Bias + tanh, the tiny
+// output layer (VALU dot products + cross-lane reduction), Gaussian sampling (Philox), log-prob and
 // entropy are fused into the epilogue.
+//
+// Weights: one flat STREAM per network.  Every hidden layer is cut into passes of 16 output tiles
+// (256 features: the 512-wide layers take two passes, so only 64 accumulators are live), and a
+// pass's k-steps are uniform blocks of 16 tiles x 64 lanes x 4 k = 1,024 floats (4 KB):
+//   layer 1: 16 k-steps (K = 52 padded to 64; k-steps 13-15 hold zeros and are never multiplied)
+//   layer 2: 2 passes x 64 k-steps, layer 3: 2 x 128, layer 4: 1 x 128          = 528 k-steps
+// The 4 waves of a workgroup (64 rows) share the stream through a double-buffered LDS ring of
+// chunks of kCK = 8 k-steps (32 KB): during chunk g every wave loads a quarter of chunk g + 1 into
+// registers (issued before chunk g's MFMAs, so the L2 / Infinity-Cache latency hides behind them),
+// writes it to the other buffer before chunk g's last k-step, and one workgroup barrier per chunk
+// publishes it.  The stream runs on across pass and layer boundaries, so no pass starts with an
+// exposed load; each pass's bias + tanh epilogue is drained between the next pass's MFMAs.  (Round 2's form restarted the staging at every pass with one serial
+// load -> wait -> LDS write per float4, and the compiler sank part of each chunk's prefetch behind
+// its MFMAs: 0.60 of the MFMA peak.)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/vss.h"
+
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "vss_policy.hip targets gfx950 (CDNA4) only"
+#endif
 
 namespace vpol {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kIn = 52, kH1 = 256, kH2 = 512, kH3 = 512, kH4 = 256;
-constexpr int kWaves = 4;          // waves per workgroup (independent; 64 rows per workgroup)
+constexpr int kWaves = 4;          // waves per workgroup (64 rows per workgroup), one per SIMD
 constexpr int kRowsPerWave = 16;
+constexpr int kTiles = 16;                         // output tiles of one pass (256 features)
+constexpr int kStepFloats = kTiles * 16 * 4;       // one pass's weights for one k-step: 1,024 floats
+constexpr int kCK = 8;                             // k-steps per chunk
+constexpr int kChunkF4 = kCK * kStepFloats / 4;    // float4 per chunk (2,048 = 32 KB)
+constexpr int kStepsL1 = 16, kStepsL2 = 64, kStepsL3 = 128, kStepsL4 = 128;
+constexpr int kUsedStepsL1 = kIn / 4;              // 13
+constexpr int kStreamSteps = kStepsL1 + 2 * kStepsL2 + 2 * kStepsL3 + kStepsL4;  // 528
+constexpr int kNetChunks = kStreamSteps / kCK;     // 66
+static_assert(kStepsL1 % kCK == 0 && kStepsL2 % kCK == 0 && kStepsL3 % kCK == 0, "passes must be whole chunks");
+constexpr int kStageF4 = kChunkF4 / (kWaves * 64);  // float4 each lane stages per chunk (8)
+// first chunk of each pass within a network's stream
+constexpr int kG1 = 0, kG2a = kStepsL1 / kCK, kG2b = kG2a + kStepsL2 / kCK, kG3a = kG2b + kStepsL2 / kCK,
+              kG3b = kG3a + kStepsL3 / kCK, kG4 = kG3b + kStepsL3 / kCK;
+static_assert(kG4 + kStepsL4 / kCK == kNetChunks, "stream layout");
 
 // packed-buffer offsets (floats) of one network with n_out outputs
-__host__ __device__ constexpr int64_t off_w1() { return 0; }
-__host__ __device__ constexpr int64_t off_w2() { return off_w1() + (int64_t)kIn * kH1; }
-__host__ __device__ constexpr int64_t off_w3() { return off_w2() + (int64_t)kH1 * kH2; }
-__host__ __device__ constexpr int64_t off_w4() { return off_w3() + (int64_t)kH2 * kH3; }
-__host__ __device__ constexpr int64_t off_w5() { return off_w4() + (int64_t)kH3 * kH4; }
+__host__ __device__ constexpr int64_t off_w5() { return (int64_t)kStreamSteps * kStepFloats; }
 __host__ __device__ constexpr int64_t off_b(int n_out) { return off_w5() + (int64_t)n_out * kH4; }
 __host__ __device__ constexpr int64_t packed_size(int n_out) {
   return off_b(n_out) + kH1 + kH2 + kH3 + kH4 + n_out;
 }
+// the packed tail past the stream (output-layer weights, then every bias): staged into LDS once per
+// workgroup, so the epilogues read it with ds_read (lgkmcnt) -- a global load there would wait, by
+// vmcnt's in-order count, for the next chunk's staging loads issued before it
+__host__ __device__ constexpr int tail_floats(int n_out) { return (int)(packed_size(n_out) - off_w5()); }
 
 // ---- packing ---------------------------------------------------------------------------------------
-// MFMA layer (K inputs, N outputs, K4 = K/4 k-steps, NT = N/16 output tiles), packed as
-// [s][q = nt/4][lane][c = nt%4]: value = W[16*nt + (lane&15)][kidx(s, lane)], with
-//   first layer:  kidx = 4s + (lane>>4)                 (inputs read from the obs rows)
-//   later layers: kidx = 16*(s>>2) + 4*(lane>>4) + (s&3) (inputs = previous accumulators)
-__device__ __forceinline__ int kidx(bool first, int s, int lane) {
-  return first ? 4 * s + (lane >> 4) : 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3);
-}
-
+// Stream k-step block (layer, pass p, k-step s): [q = 0..3][lane][c = 0..3], value
+// W[16 nt + (lane & 15)][kidx(s, lane)] with nt = 16 p + 4 q + c, and
+//   layer 1:      kidx = 4 s + (lane >> 4)                    (inputs read from the obs rows)
+//   later layers: kidx = 16 (s >> 2) + 4 (lane >> 4) + (s & 3) (inputs = previous accumulators)
+// (zero for kidx >= K: layer 1's padding).
 __global__ void pack_kernel(int n_out, const float* __restrict__ w1, const float* __restrict__ b1,
                             const float* __restrict__ w2, const float* __restrict__ b2,
                             const float* __restrict__ w3, const float* __restrict__ b3,
@@ -58,21 +85,19 @@ __global__ void pack_kernel(int n_out, const float* __restrict__ w1, const float
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     float v;
     if (e < off_w5()) {
+      int blk = (int)(e / kStepFloats);
+      const int i = (int)(e % kStepFloats);
+      const int c = i & 3, lane = (i >> 2) & 63, q = i >> 8;
       const float* w;
-      int K, N;
-      int64_t base;
+      int K, s, p = 0;
       bool first = false;
-      if (e < off_w2()) { w = w1; K = kIn; N = kH1; base = off_w1(); first = true; }
-      else if (e < off_w3()) { w = w2; K = kH1; N = kH2; base = off_w2(); }
-      else if (e < off_w4()) { w = w3; K = kH2; N = kH3; base = off_w3(); }
-      else { w = w4; K = kH3; N = kH4; base = off_w4(); }
-      const int64_t i = e - base;
-      const int NQ = N / 64;  // float4 groups of output tiles
-      const int c = (int)(i & 3), lane = (int)((i >> 2) & 63);
-      const int64_t sq = i >> 8;
-      const int q = (int)(sq % NQ), s = (int)(sq / NQ);
-      const int nt = 4 * q + c;
-      v = w[(int64_t)(16 * nt + (lane & 15)) * K + kidx(first, s, lane)];
+      if (blk < kStepsL1) { w = w1; K = kIn; s = blk; first = true; }
+      else if ((blk -= kStepsL1) < 2 * kStepsL2) { w = w2; K = kH1; p = blk / kStepsL2; s = blk % kStepsL2; }
+      else if ((blk -= 2 * kStepsL2) < 2 * kStepsL3) { w = w3; K = kH2; p = blk / kStepsL3; s = blk % kStepsL3; }
+      else { blk -= 2 * kStepsL3; w = w4; K = kH3; s = blk; }
+      const int nt = kTiles * p + 4 * q + c;
+      const int k = first ? 4 * s + (lane >> 4) : 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3);
+      v = k < K ? w[(int64_t)(16 * nt + (lane & 15)) * K + k] : 0.0f;
     } else if (e < off_b(n_out)) {  // output layer: [a][g][t][r] = W5[a][16t + 4g + r]
       const int64_t i = e - off_w5();
       const int a = (int)(i / kH4), rem = (int)(i % kH4);
@@ -97,137 +122,122 @@ __device__ __forceinline__ float fast_tanh(float x) {
   return copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), x);
 }
 
-// ---- one MFMA layer: hout = tanh(W . hin + b), all in registers ------------------------------------
-// The 4 waves of a workgroup (64 rows) share every weight chunk through LDS: a chunk = CK
-// k-steps x (N / OS) outputs, double-buffered.  Each wave loads a quarter of chunk c+1 from L2
-// into registers while it runs the MFMAs of chunk c out of LDS, then writes it to the other LDS
-// buffer; one workgroup barrier per chunk.  L2 weight traffic is 1/4 of the per-wave streaming
-// form.  OS > 1 computes the outputs in OS passes of N / OS (each weight is still read once; the
-// inputs stay in registers): OS x fewer live accumulators, which is what keeps the 512-wide layers
-// out of scratch.  All loops are unrolled (hin / acc indices static).
-#ifndef VPOL_CK
-#define VPOL_CK 8
-#endif
-#ifndef VPOL_OS
-#define VPOL_OS 2
-#endif
-constexpr int kCK = VPOL_CK;                               // k-steps per chunk
-constexpr int kOS512 = VPOL_OS;                            // output passes of the 512-wide layers
-constexpr int kChunkFloats = kCK * (kH2 / kOS512 > kH1 ? kH2 / kOS512 : kH1) * 4;  // largest chunk (floats)
+// ---- the weight stream ------------------------------------------------------------------------------
+// Chunk g of a launch's stream (one network's kNetChunks chunks).  Every chunk index below is a
+// compile-time constant once the pass loops are unrolled.
+struct Stream {
+  const f32x4* net;
+  f32x4* lds;  // two chunk buffers
+  int wave, lane, last;
+  f32x4 stage[kStageF4];
+  f32x4 first[4];  // the weights of the current chunk's first k-step (read before it starts)
 
-template <int K4, int NT, int OS>
-__device__ __forceinline__ void mfma_layer(const float* __restrict__ wp, const float* __restrict__ bias,
-                                           const float (&hin)[K4], float (&hout)[NT * 4], int lane,
-                                           float* __restrict__ lds, int wave) {
-  static_assert(NT % (4 * OS) == 0, "passes must split whole float4 groups");
-  constexpr int NQ = NT / 4;                         // float4 weight groups per k-step (layer)
-  constexpr int NTP = NT / OS, NQP = NQ / OS;        // tiles / groups per pass
-  constexpr int NCH = (K4 + kCK - 1) / kCK;          // chunks per pass
-  constexpr int CH_F4 = kCK * NQP * 64;              // float4 per full chunk
-  static_assert(CH_F4 * 4 <= kChunkFloats, "chunk must fit one LDS buffer");
-  constexpr int PER_WAVE = (CH_F4 + 3) / 4;          // float4 each wave stages per chunk
-  constexpr int PER_LANE = (PER_WAVE + 63) / 64;
-  const f32x4* g4 = reinterpret_cast<const f32x4*>(wp);
-  f32x4* l4 = reinterpret_cast<f32x4*>(lds);
-  const int g = lane >> 4;
-  // chunk element e (= (u * NQP + qq) * 64 + l) of chunk c of pass p -> packed float4 index
-  auto gidx = [&](int p, int c, int e) {
-    const int u = e / (NQP * 64), rest = e - u * (NQP * 64);
-    return ((c * kCK + u) * NQ + p * NQP) * 64 + rest;
-  };
-  auto in_layer = [&](int c, int e) { return c * kCK + e / (NQP * 64) < K4; };
+  __device__ __forceinline__ void load(int g) {
+    const f32x4* src = net + (int64_t)g * kChunkF4;
 #pragma unroll
-  for (int p = 0; p < OS; ++p) {
-    f32x4 acc[NTP];
+    for (int j = 0; j < kStageF4; ++j) stage[j] = src[(wave * kStageF4 + j) * 64 + lane];
+  }
+  __device__ __forceinline__ void store(int g) {
+    f32x4* dst = lds + (g & 1) * kChunkF4;
 #pragma unroll
-    for (int nt = 0; nt < NTP; ++nt) acc[nt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    f32x4 stage[PER_LANE];
-    // chunk 0 -> buffer 0: every load issued before the first LDS write (one wait, not one per load)
+    for (int j = 0; j < kStageF4; ++j) dst[(wave * kStageF4 + j) * 64 + lane] = stage[j];
+  }
+};
+
+// One pass of NSTEPS k-steps (the first NUSED multiplied) into kTiles output tiles, out of the
+// stream's chunks g0, g0 + 1, ...: hin holds the layer's B operands (one per k-step); the raw
+// accumulators are left in acc.  Their bias + tanh epilogue is DEFERRED into the next pass, which
+// drains it tile by tile between its own MFMAs (one wave per SIMD: nothing else would hide that VALU
+// work): with DRAIN, pend holds the previous pass's accumulators and tile j becomes
+// pdst[4 (DT0 + j) + r] = tanh(pend[j][r] + pbias[16 (DT0 + j) + 4 (lane >> 4) + r]) -- tile 0 before
+// the first k-step, tile j after k-step j - 1.  When pdst is this pass's own hin (the previous
+// layer's last pass), k-step s reads tile s >> 2, which has been drained by then.
+__device__ __forceinline__ void drain_tile(const f32x4& pend, const float* pbias, float* dst, int grp) {
+  const f32x4 bb = *reinterpret_cast<const f32x4*>(pbias + 4 * grp);  // LDS
 #pragma unroll
-    for (int j = 0; j < PER_LANE; ++j) {
-      const int e = wave * PER_WAVE + j * 64 + lane;
-      if (e < (wave + 1) * PER_WAVE && e < CH_F4 && in_layer(0, e)) stage[j] = g4[gidx(p, 0, e)];
-    }
-    __builtin_amdgcn_sched_barrier(0);
+  for (int r = 0; r < 4; ++r) dst[r] = fast_tanh(pend[r] + bb[r]);
+}
+
+template <int NSTEPS, int NUSED, bool DRAIN, int DT0, int KIN, int NDST>
+__device__ __forceinline__ void mfma_pass(Stream& st, int g0, const float (&hin)[KIN], f32x4 (&acc)[kTiles],
+                                          const f32x4 (&pend)[kTiles], const float* pbias, float (&pdst)[NDST]) {
+  static_assert(NSTEPS % kCK == 0 && NUSED <= NSTEPS && NUSED <= KIN, "pass shape");
+  static_assert(!DRAIN || (NUSED >= kTiles && 4 * (DT0 + kTiles) <= NDST), "drain shape");
+  constexpr int NCH = NSTEPS / kCK;
+  const int lane = st.lane, grp = lane >> 4;
 #pragma unroll
-    for (int j = 0; j < PER_LANE; ++j) {
-      const int e = wave * PER_WAVE + j * 64 + lane;
-      if (e < (wave + 1) * PER_WAVE && e < CH_F4 && in_layer(0, e)) l4[e] = stage[j];
-    }
-    __syncthreads();
+  for (int nt = 0; nt < kTiles; ++nt) acc[nt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  if constexpr (DRAIN) drain_tile(pend[0], pbias + 16 * DT0, pdst + 4 * DT0, grp);
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int buf = c & 1;
-      // stage chunk c+1 (L2 -> registers) while chunk c computes
-      if (c + 1 < NCH) {
+  for (int c = 0; c < NCH; ++c) {
+    const int g = g0 + c;
+    const bool more = g + 1 <= st.last;
+    const int uc = NUSED - c * kCK < kCK ? NUSED - c * kCK : kCK;  // k-steps of this chunk multiplied
+    if (more) st.load(g + 1);  // the next chunk (possibly the next pass's / network's), L2 -> registers
+    __builtin_amdgcn_sched_barrier(0);  // keep those loads ahead of this chunk's MFMAs
+    const f32x4* cur = st.lds + (g & 1) * kChunkF4;
+    // the weights of k-step u + 1 are read from LDS while k-step u's MFMAs run (two register sets)
+    f32x4 wk[4], wn[4];
 #pragma unroll
-        for (int j = 0; j < PER_LANE; ++j) {
-          const int e = wave * PER_WAVE + j * 64 + lane;
-          if (e < (wave + 1) * PER_WAVE && e < CH_F4 && in_layer(c + 1, e)) stage[j] = g4[gidx(p, c + 1, e)];
+    for (int q = 0; q < 4; ++q) wk[q] = st.first[q];
+#pragma unroll
+    for (int u = 0; u < kCK; ++u) {
+      const int s = c * kCK + u;
+      if (u < uc) {
+        if (u + 1 < uc) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) wn[q] = cur[((u + 1) * 4 + q) * 64 + lane];
+        } else if (more) {
+          // Before the chunk's last k-step (whose weights are in registers): publish chunk g + 1 --
+          // its buffer was last read before the previous chunk's barrier -- and read its first k-step
+          // while this k-step's MFMAs run, so the next chunk starts without an LDS round trip.  Every
+          // LDS read of chunk g has completed (the barrier's fence), so the buffer is free after it.
+          st.store(g + 1);
+          __syncthreads();
+          const f32x4* nxt = st.lds + ((g + 1) & 1) * kChunkF4;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) st.first[q] = nxt[q * 64 + lane];
         }
-      }
-      __builtin_amdgcn_sched_barrier(0);  // the next chunk's loads stay ahead of this chunk's MFMAs
-      const f32x4* cur = l4 + buf * (kChunkFloats / 4);
-      // the weights of k-step u + 1 are read from LDS while k-step u's MFMAs run (two register
-      // sets), so the LDS latency hides behind NQP x 4 MFMAs instead of stalling every group
-      f32x4 wk[NQP], wn[NQP];
+        // keep those LDS reads ahead of this k-step's MFMAs (the scheduler would sink them to their
+        // use); VALU / SALU / transcendental / global-memory work may still move across
+        __builtin_amdgcn_sched_barrier(0x416);
 #pragma unroll
-      for (int q = 0; q < NQP; ++q) wk[q] = cur[q * 64 + lane];
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int u = 0; u < kCK; ++u) {
-        const int s = c * kCK + u;
-        if (s < K4) {
-          if (u + 1 < kCK && s + 1 < K4) {
-#pragma unroll
-            for (int q = 0; q < NQP; ++q) wn[q] = cur[((u + 1) * NQP + q) * 64 + lane];
-          }
-          // keep those LDS reads ahead of this k-step's MFMAs (the scheduler would sink them to
-          // their use); VALU / SALU / transcendental / global-memory work may still move across
-          __builtin_amdgcn_sched_barrier(0x416);
-#pragma unroll
-          for (int q = 0; q < NQP; ++q)
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc)
-              acc[4 * q + cc] = __builtin_amdgcn_mfma_f32_16x16x4f32(wk[q][cc], hin[s], acc[4 * q + cc], 0, 0, 0);
-#pragma unroll
-          for (int q = 0; q < NQP; ++q) wk[q] = wn[q];
+          for (int cc = 0; cc < 4; ++cc)
+            acc[4 * q + cc] = __builtin_amdgcn_mfma_f32_16x16x4f32(wk[q][cc], hin[s], acc[4 * q + cc], 0, 0, 0);
+        if constexpr (DRAIN) {
+          if (s + 1 < kTiles) drain_tile(pend[s + 1], pbias + 16 * (DT0 + s + 1), pdst + 4 * (DT0 + s + 1), grp);
         }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wk[q] = wn[q];
       }
-      if (c + 1 < NCH) {
-        f32x4* nxt = l4 + (buf ^ 1) * (kChunkFloats / 4);
-#pragma unroll
-        for (int j = 0; j < PER_LANE; ++j) {
-          const int e = wave * PER_WAVE + j * 64 + lane;
-          if (e < (wave + 1) * PER_WAVE && e < CH_F4 && in_layer(c + 1, e)) nxt[e] = stage[j];
-        }
-      }
-      __syncthreads();
-    }
-#pragma unroll
-    for (int nt = 0; nt < NTP; ++nt) {
-      const int tile = p * NTP + nt;
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + 16 * tile + 4 * g);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) hout[4 * tile + r] = fast_tanh(acc[nt][r] + bb[r]);
     }
   }
 }
 
-// Full network on this wave's 16 rows; returns the n_out outputs of sample (lane & 15) in every
-// lane of its group (the reduction over the 4 lane groups is broadcast).
+// One network on this wave's 16 rows, its stream chunks starting at g0, its packed tail (output
+// weights + biases, tail_floats) in LDS at `tail`; returns the NOUT outputs of sample (lane & 15) in
+// every lane of its group (the reduction over the 4 lane groups is broadcast).  Passes alternate
+// between two accumulator sets: each pass drains the previous one's epilogue.
 template <int NOUT>
-__device__ __forceinline__ void mlp(const float* __restrict__ packed, const float (&x)[13], float (&out)[NOUT],
-                                    int lane, float* lds, int wave) {
-  const float* bias = packed + off_b(NOUT);
+__device__ __forceinline__ void mlp(Stream& st, int g0, const float* tail, const float (&x)[16], float (&out)[NOUT]) {
+  const float* bias = tail + NOUT * kH4;
+  const float *b1 = bias, *b2 = b1 + kH1, *b3 = b2 + kH2, *b4 = b3 + kH3;
   float h1[64], h2[128], h3[128], h4[64];
-  mfma_layer<13, 16, 1>(packed + off_w1(), bias, x, h1, lane, lds, wave);
-  mfma_layer<64, 32, kOS512>(packed + off_w2(), bias + kH1, h1, h2, lane, lds, wave);
-  mfma_layer<128, 32, kOS512>(packed + off_w3(), bias + kH1 + kH2, h2, h3, lane, lds, wave);
-  mfma_layer<128, 16, 1>(packed + off_w4(), bias + kH1 + kH2 + kH3, h3, h4, lane, lds, wave);
-  const int g = lane >> 4;
+  f32x4 A[kTiles], B[kTiles];
+  mfma_pass<kStepsL1, kUsedStepsL1, false, 0>(st, g0 + kG1, x, A, B, b1, h1);        // B unused
+  mfma_pass<kStepsL2, kStepsL2, true, 0>(st, g0 + kG2a, h1, B, A, b1, h1);           // drains h1
+  mfma_pass<kStepsL2, kStepsL2, true, 0>(st, g0 + kG2b, h1, A, B, b2, h2);           // h2 tiles 0-15
+  mfma_pass<kStepsL3, kStepsL3, true, kTiles>(st, g0 + kG3a, h2, B, A, b2, h2);      // h2 tiles 16-31
+  mfma_pass<kStepsL3, kStepsL3, true, 0>(st, g0 + kG3b, h2, A, B, b3, h3);           // h3 tiles 0-15
+  mfma_pass<kStepsL4, kStepsL4, true, kTiles>(st, g0 + kG4, h3, B, A, b3, h3);       // h3 tiles 16-31
+  const int g = st.lane >> 4;
+#pragma unroll
+  for (int nt = 0; nt < kTiles; ++nt) drain_tile(B[nt], b4 + 16 * nt, h4 + 4 * nt, g);  // the last pass: eager
 #pragma unroll
   for (int a = 0; a < NOUT; ++a) {
-    const f32x4* w = reinterpret_cast<const f32x4*>(packed + off_w5() + (int64_t)a * kH4 + 64 * g);
+    const f32x4* w = reinterpret_cast<const f32x4*>(tail + a * kH4 + 64 * g);
     float acc = 0.0f;
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
@@ -241,12 +251,13 @@ __device__ __forceinline__ void mlp(const float* __restrict__ packed, const floa
   }
 }
 
+// the first layer's B operands: x[s] = obs[row][4 s + (lane >> 4)] (s < 13; the padding k-steps 0)
 __device__ __forceinline__ void load_rows(const float* __restrict__ obs, int64_t rows, int64_t r0, int lane,
-                                          float (&x)[13]) {
+                                          float (&x)[16]) {
   const int64_t row = r0 + (lane & 15);
   const int g = lane >> 4;
 #pragma unroll
-  for (int s = 0; s < 13; ++s) x[s] = row < rows ? obs[row * kIn + 4 * s + g] : 0.0f;
+  for (int s = 0; s < 16; ++s) x[s] = (s < kUsedStepsL1 && row < rows) ? obs[row * kIn + 4 * s + g] : 0.0f;
 }
 
 // Philox4x32-10 (same constants as the step kernel); one standard normal pair per call.
@@ -286,27 +297,46 @@ struct PolicyArgs {
   const int64_t* row_mask;  // critic-only: evaluate / write only rows with row_mask[row] != 0
 };
 
-// get_action_and_value (ppo…:157-164): actor mean, Normal(mean, exp(logstd)) sample (or the given
-// action), log-prob and entropy summed over action dims, critic value.  CRITIC_ONLY: get_value.
-template <int NACT, bool CRITIC_ONLY>
+// get_action_and_value (ppo…:157-164) as two launches over the same rows, one network each:
+// ACTOR = true: actor mean, Normal(mean, exp(logstd)) sample (or the given action), log-prob and
+// entropy summed over action dims; ACTOR = false: the critic's value (Agent.get_value; with row_mask,
+// only the masked rows).  One network per launch keeps the weight stream that the concurrently running
+// workgroups read at 2.1 MB, inside one XCD's 4 MB L2 (actor + critic in one launch stream 4.3 MB and
+// measured 2.6 % slower: profiles/r03f_policy_bench.log).
+template <int NACT, bool ACTOR>
 __global__ __launch_bounds__(kWaves * 64) void policy_kernel(PolicyArgs p) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * kChunkFloats];
+  constexpr int NOUT = ACTOR ? NACT : 1;
+  __shared__ __attribute__((aligned(16))) f32x4 lds[2 * kChunkF4];
+  __shared__ __attribute__((aligned(16))) float tails[tail_floats(NOUT)];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t r0 = ((int64_t)blockIdx.x * kWaves + wave) * kRowsPerWave;
   // waves past the last row still take part in the weight staging and barriers
-  if (CRITIC_ONLY && p.row_mask) {
+  if (!ACTOR && p.row_mask) {
     // masked terminal-value pass: a workgroup with no masked row has nothing to do (uniform exit)
     const int64_t wr = (int64_t)blockIdx.x * kWaves * kRowsPerWave + threadIdx.x;
     const bool m = threadIdx.x < kWaves * kRowsPerWave && wr < p.rows && p.row_mask[wr] != 0;
     if (__syncthreads_or(m) == 0) return;
   }
-  float x[13];
+  const float* net = ACTOR ? p.actor : p.critic;
+  Stream st;
+  st.net = reinterpret_cast<const f32x4*>(net);
+  st.lds = lds;
+  st.wave = wave;
+  st.lane = lane;
+  st.last = kNetChunks - 1;
+  st.load(0);  // the stream's first chunk
+  float x[16];
   load_rows(p.obs, p.rows, r0, lane, x);
+  for (int i = threadIdx.x; i < tail_floats(NOUT); i += kWaves * 64) tails[i] = net[off_w5() + i];
+  st.store(0);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) st.first[q] = lds[q * 64 + lane];
   const int64_t row = r0 + (lane & 15);
   const bool writer = (lane >> 4) == 0 && row < p.rows;
-  if constexpr (!CRITIC_ONLY) {
-    float mean[NACT];
-    mlp<NACT>(p.actor, x, mean, lane, lds, wave);
+  float out[NOUT];
+  mlp<NOUT>(st, 0, tails, x, out);
+  if constexpr (ACTOR) {
     if (writer) {
       // torch.distributions.Normal: log_prob = -(a-mu)^2/(2 var) - log(scale) - log(sqrt(2 pi));
       // entropy = 0.5 + 0.5 log(2 pi) + log(scale)
@@ -318,23 +348,22 @@ __global__ __launch_bounds__(kWaves * 64) void policy_kernel(PolicyArgs p) {
 #pragma unroll
         for (int h = 0; h < 2 && a + h < NACT; ++h) {
           const float scale = expf(p.logstd[a + h]);
-          const float act = p.action_in ? p.action_in[row * NACT + a + h] : mean[a + h] + scale * (h ? z1 : z0);
-          const float d = act - mean[a + h];
+          const float act = p.action_in ? p.action_in[row * NACT + a + h] : out[a + h] + scale * (h ? z1 : z0);
+          const float d = act - out[a + h];
           const float log_scale = logf(scale);
           lp += -(d * d) / (2.0f * (scale * scale)) - log_scale - 0.91893853320467274f;
           ent += 0.5f + 0.91893853320467274f + log_scale;
           if (p.action_out) p.action_out[row * NACT + a + h] = act;
-          if (p.mean_out) p.mean_out[row * NACT + a + h] = mean[a + h];
+          if (p.mean_out) p.mean_out[row * NACT + a + h] = out[a + h];
         }
       }
       if (p.logprob_out) p.logprob_out[row] = lp;
       if (p.entropy_out) p.entropy_out[row] = ent;
     }
+  } else {
+    const bool masked_out = p.row_mask && writer && p.row_mask[row] == 0;
+    if (writer && !masked_out && p.value_out) p.value_out[row] = out[0];
   }
-  float v[1];
-  mlp<1>(p.critic, x, v, lane, lds, wave);
-  const bool masked_out = CRITIC_ONLY && p.row_mask && writer && p.row_mask[row] == 0;
-  if (writer && !masked_out && p.value_out) p.value_out[row] = v[0];
 }
 
 }  // namespace vpol
@@ -381,9 +410,11 @@ int vss_value_forward_masked(void* stream, int64_t rows, int32_t n_act, const fl
   const int64_t waves = (rows + vpol::kRowsPerWave - 1) / vpol::kRowsPerWave;
   const dim3 grid((unsigned)((waves + vpol::kWaves - 1) / vpol::kWaves)), block(vpol::kWaves * 64);
   hipStream_t s = (hipStream_t)stream;
-  if (critic_only) hipLaunchKernelGGL((vpol::policy_kernel<2, true>), grid, block, 0, s, a);
-  else if (n_act == 2) hipLaunchKernelGGL((vpol::policy_kernel<2, false>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((vpol::policy_kernel<6, false>), grid, block, 0, s, a);
+  if (!critic_only) {
+    if (n_act == 2) hipLaunchKernelGGL((vpol::policy_kernel<2, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((vpol::policy_kernel<6, true>), grid, block, 0, s, a);
+  }
+  hipLaunchKernelGGL((vpol::policy_kernel<1, false>), grid, block, 0, s, a);
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 

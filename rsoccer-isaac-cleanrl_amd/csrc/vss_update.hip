@@ -133,7 +133,11 @@ namespace vgemm {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-enum { EPI_TANH = 0, EPI_DTANH = 1 };
+// EPI_TANH_OUT: EPI_TANH for the last hidden layer (n = 256, a block holds whole rows) plus the
+// output layer folded in (ppo…:104-111's last nn.Linear): the block also writes, per 64-column wave
+// slice, the partial dot products of its tanh rows with the output layer's weight
+// (out_part[slice][row][a], a < KO), so out = sum over the 4 slices + bias without reading y again.
+enum { EPI_TANH = 0, EPI_DTANH = 1, EPI_TANH_OUT = 2 };
 
 // tanh(z): odd Taylor polynomial to z^9 for |z| < 0.3 (truncation < 0.6 ulp there; the exponential
 // form below would cancel in 1 - t), else sign(z) (1 - t) / (1 + t), t = 2^(-2|z| log2 e), on the
@@ -179,7 +183,24 @@ struct GemmArgs {
   float* out;         // (rows, n)
   float* partial;     // EPI_DTANH: (G / (n / BN), n) column sums of out
   int64_t tiles;      // ceil(rows / BM) * (n / BN) output tiles, row band major
+  const float* w_out; // EPI_TANH_OUT: the output layer's weight (KO, n)
+  float* out_part;    // EPI_TANH_OUT: (n / 64, rows, KO) partial output-layer sums
 };
+
+// Sum over the 16 lanes of a DPP row (lanes 16r .. 16r + 15): xor 1 and 2 by quad permutes, then the
+// half-row and row mirrors (which act as xor 4 and xor 8 once every quad, then every half, is
+// uniform); every lane of the row ends with the row's sum, added in one fixed order.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f32<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_f32<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_f32<0x141>(v);  // row_half_mirror
+  v += dpp_f32<0x140>(v);  // row_mirror
+  return v;
+}
 
 // One wave's (TM x 32) x 64 output block, 32 x 64 at a time through the wave's LDS scratch (32 x kES
 // floats), so that every global access is a 16-B piece of a 256-B row segment.  C/D map of a 32x32
@@ -187,12 +208,13 @@ struct GemmArgs {
 // two row halves of a ds_write_b32 land 32 banks apart and each 16-lane ds_read_b128 group reads 64
 // consecutive dwords (conflict-free both ways).  EPI_TANH: out = tanh(acc + bias); EPI_DTANH:
 // out = acc * (1 - y^2) and csum += out (this lane's 4 columns).
-template <int EPI, int TM, int TN, bool MASK = true>
+template <int EPI, int TM, int TN, bool MASK = true, int KO = 0>
 __device__ __forceinline__ void store_tile(const GemmArgs& p, f32x16 (&acc)[TM][TN], float* scr, int64_t rowb0, int colw,
-                                           float4& csum) {
+                                           float4& csum, const float* wo_lds = nullptr) {
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int er = lane >> 4, ec = (lane & 15) * 4;  // reader: rows er + 4q, columns ec..ec+3
   const int64_t M = p.rows;
+  static_assert(EPI != EPI_TANH_OUT || (KO > 0 && !MASK), "EPI_TANH_OUT: exact shapes, KO output columns");
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int64_t rowb = rowb0 + i * 32;
@@ -210,11 +232,11 @@ __device__ __forceinline__ void store_tile(const GemmArgs& p, f32x16 (&acc)[TM][
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const float bcol = EPI == EPI_TANH ? p.bias[colw + j * 32 + r] : 0.0f;
+      const float bcol = EPI != EPI_DTANH ? p.bias[colw + j * 32 + r] : 0.0f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         float v = acc[i][j][e];
-        if constexpr (EPI == EPI_TANH) v = tanh_f32(v + bcol);
+        if constexpr (EPI != EPI_DTANH) v = tanh_f32(v + bcol);
         scr[((e & 3) + 8 * (e >> 2) + 4 * h) * kES + j * 32 + r] = v;
       }
     }
@@ -240,6 +262,22 @@ __device__ __forceinline__ void store_tile(const GemmArgs& p, f32x16 (&acc)[TM][
                                       reinterpret_cast<vupd::f32x4*>(p.out + row * p.n + colw + ec));
         } else {
           *reinterpret_cast<float4*>(p.out + row * p.n + colw + ec) = v;
+        }
+      }
+      if constexpr (EPI == EPI_TANH_OUT) {
+        // the output layer on this row's 64 columns of the slice: 4 products per lane, then the 16
+        // lanes of the row; one lane writes the slice's partial sums (fixed order: deterministic)
+#pragma unroll
+        for (int a = 0; a < KO; ++a) {
+          // the output weights of this lane's 4 columns, from the LDS copy (a global load here would
+          // wait, by vmcnt's in-order count, for the K tiles prefetched behind it)
+          const vupd::f32x4 wo = *reinterpret_cast<const vupd::f32x4*>(wo_lds + a * 256 + colw + ec);
+          float d = v.x * wo[0];
+          d = fmaf(v.y, wo[1], d);
+          d = fmaf(v.z, wo[2], d);
+          d = fmaf(v.w, wo[3], d);
+          d = row16_sum(d);
+          if ((lane & 15) == 0) p.out_part[((int64_t)(colw >> 6) * M + row) * KO + a] = d;
         }
       }
     }
@@ -415,10 +453,14 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel(Gemm
 // write R[(g + 1) & 1] (= K tile g + 1) into LDS[(g + 1) & 1]; barrier; load K tile g + 3 into
 // R[(g + 1) & 1].  The fetch cursor advances its pointers by one K tile (32 floats) per load and
 // recomputes them only at a tile change.
-template <int EPI, class C>
+template <int EPI, class C, int KO = 0>
 __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel_d2(GemmArgs p) {
   constexpr int BM = C::BM, BN = C::BN, TM = C::TM, TN = C::TN, LROWS = C::LROWS, RA = C::RA, RB = C::RB;
+  static_assert(EPI != EPI_TANH_OUT || BN == 256, "EPI_TANH_OUT: blocks of whole 256-wide rows");
   __shared__ float lds[C::LDSF];
+  __shared__ float wo_lds[KO > 0 ? KO * 256 : 1];  // EPI_TANH_OUT: the output layer's weight (KO, 256)
+  if constexpr (KO > 0)
+    for (int i = threadIdx.x; i < KO * 256; i += C::THREADS) wo_lds[i] = p.w_out[i];  // published by the first barrier
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv / C::WN, wn = wv % C::WN;
   const int nb = p.n / BN;
   const int K = p.k, ktiles = K / kKS;  // even (K % 64 == 0)
@@ -530,8 +572,8 @@ __global__ __launch_bounds__(C::THREADS, C::BLOCKS_PER_CU) void gemm_kernel_d2(G
     // backward, exact shapes: no row masks (their branches made the compiler drain vmcnt to 0, i.e.
     // wait for the K tiles prefetched two ahead, at every y load; the forward measured ~1 % slower
     // without them, profiles/r02_gemm_epilogue_variants.log)
-    store_tile<EPI, TM, TN, EPI != EPI_DTANH>(p, acc, lds + (BM + BN) * kLS + wv * (32 * kES), row0 + wm * C::WROWS,
-                                              col0 + wn * C::WCOLS, csum);
+    store_tile<EPI, TM, TN, EPI == EPI_TANH, KO>(p, acc, lds + (BM + BN) * kLS + wv * (32 * kES),
+                                                 row0 + wm * C::WROWS, col0 + wn * C::WCOLS, csum, wo_lds);
     if (!has_next) break;
     __syncthreads();  // the next tile's second K tile is written into LDS 1 (the scratch)
     tile = next;
@@ -855,8 +897,27 @@ int vss_linear_tanh(void* stream, int64_t rows, int32_t k_in, int32_t n_out, con
                          rows, k_in, x, w, bias, y);
     return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
   }
-  const vgemm::GemmArgs a{rows, n_out, k_in, x, w, bias, nullptr, y, nullptr, 0};
+  const vgemm::GemmArgs a{rows, n_out, k_in, x, w, bias, nullptr, y, nullptr, 0, nullptr, nullptr};
   return vgemm::launch<vgemm::EPI_TANH>(stream, a, vgemm::plan(rows, k_in, n_out, true));
+}
+
+int vss_linear_tanh_out(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
+                        const float* bias, float* y, int32_t k_out, const float* w_out, float* out_part) {
+  if (!vgemm::shape_ok(rows, k_in, n_out) || misaligned(x) || misaligned(w) || misaligned(y) || !bias ||
+      misaligned(w_out) || !out_part)
+    return VSS_E_ARG;
+  // the forward's 256 x 256 blocks (whole 256-wide rows per block), exact shapes only
+  if (n_out != 256 || rows % 256 != 0 || k_in % 64 != 0 || !(k_out == 1 || k_out == 2 || k_out == 6)) return VSS_E_ARG;
+  if (rows == 0) return VSS_OK;
+  const vgemm::Plan pl = vgemm::plan(rows, k_in, n_out, true);
+  if (pl.kind != 1) return VSS_E_ARG;
+  vgemm::GemmArgs a{rows, n_out, k_in, x, w, bias, nullptr, y, nullptr, pl.tiles, w_out, out_part};
+  const dim3 grid((unsigned)pl.grid), block(vgemm::Cfg256::THREADS);
+  hipStream_t s = (hipStream_t)stream;
+  if (k_out == 1) hipLaunchKernelGGL((vgemm::gemm_kernel_d2<vgemm::EPI_TANH_OUT, vgemm::Cfg256, 1>), grid, block, 0, s, a);
+  else if (k_out == 2) hipLaunchKernelGGL((vgemm::gemm_kernel_d2<vgemm::EPI_TANH_OUT, vgemm::Cfg256, 2>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((vgemm::gemm_kernel_d2<vgemm::EPI_TANH_OUT, vgemm::Cfg256, 6>), grid, block, 0, s, a);
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 
 int64_t vss_linear_tanh_backward_chunks(int64_t rows, int32_t k_next, int32_t n_out) {
@@ -884,7 +945,7 @@ int vss_linear_tanh_backward(void* stream, int64_t rows, int32_t k_next, int32_t
                          w_next_t, y, grad_in, bias_partial, sp.rows_per_block);
     return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
   }
-  const vgemm::GemmArgs a{rows, n_out, k_next, grad_next, w_next_t, nullptr, y, grad_in, bias_partial, 0};
+  const vgemm::GemmArgs a{rows, n_out, k_next, grad_next, w_next_t, nullptr, y, grad_in, bias_partial, 0, nullptr, nullptr};
   return vgemm::launch<vgemm::EPI_DTANH>(stream, a, vgemm::plan(rows, k_next, n_out, false));
 }
 

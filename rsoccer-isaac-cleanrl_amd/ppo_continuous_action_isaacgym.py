@@ -34,8 +34,8 @@ from torch.distributions.normal import Normal
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from envs._gym import Box, ObservationWrapper  # noqa: E402
-from vss_amd.update import (gemm_shape_ok, linear_tanh, linear_tanh_backward, output_backward,  # noqa: E402
-                            output_backward_ok, tanh_grad_bias)
+from vss_amd.update import (gemm_shape_ok, linear_tanh, linear_tanh_backward, linear_tanh_out,  # noqa: E402
+                            linear_tanh_out_ok, output_backward, output_backward_ok, tanh_grad_bias)
 
 
 def strtobool(x: str) -> bool:
@@ -205,10 +205,17 @@ class _TanhMLP(torch.autograd.Function):
     def forward(ctx, x, *params):
         ws, bs = params[0::2], params[1::2]
         hs = [x]
-        for w, b in zip(ws[:-1], bs[:-1]):
+        for w, b in zip(ws[:-2], bs[:-2]):
             hs.append(linear_tanh(hs[-1], w, b))
+        if x.is_cuda and OUTPUT_FWD and linear_tanh_out_ok(x.shape[0], ws[-2].shape[1], ws[-2].shape[0], ws[-1].shape[0]):
+            # the last hidden layer and the output layer in one launch (vss_linear_tanh_out)
+            h, out = linear_tanh_out(hs[-1], ws[-2], bs[-2], ws[-1], bs[-1])
+            hs.append(h)
+        else:
+            hs.append(linear_tanh(hs[-1], ws[-2], bs[-2]))
+            out = torch.addmm(bs[-1], hs[-1], ws[-1].t())
         ctx.save_for_backward(*hs, *ws)
-        return torch.addmm(bs[-1], hs[-1], ws[-1].t())
+        return out
 
     @staticmethod
     def backward(ctx, gout):
@@ -247,6 +254,9 @@ UPDATE_MLP = os.environ.get("VSS_UPDATE_MLP", "fused")
 # the fused path's output layer: "1" (default) = its backward and weight gradient in one streaming
 # pass (vss_output_backward), "0" = the padded backward + a split-K dW GEMM (A/B switch)
 OUTPUT_BWD = os.environ.get("VSS_OUTPUT_BWD", "1") == "1"
+# ... and its forward: "1" (default) = folded into the last hidden layer's GEMM epilogue
+# (vss_linear_tanh_out) where the shapes allow, "0" = a separate addmm (A/B switch)
+OUTPUT_FWD = os.environ.get("VSS_OUTPUT_FWD", "1") == "1"
 
 
 def _fused_mlp_ok(seq: nn.Sequential) -> bool:
@@ -573,7 +583,10 @@ def local_device_index() -> int:
     return int(os.environ.get("VSS_LOCAL_DEVICE", os.environ.get("LOCAL_RANK", "0")))
 
 
-def train(args):
+def train(args, on_update=None):
+    """The PPO loop (ppo…:231-379).  on_update(record, agent) -- optional, called after every update
+    with that update's history record -- may return True to stop training early (tools/time_to_score.py
+    evaluates the live policy there)."""
     world, rank, local = setup_distributed()
     run_name = f"{args.exp_name}_ppo-{args.env_id}_{args.seed}"
     writer = make_writer(args, run_name, rank)
@@ -699,6 +712,8 @@ def train(args):
         if rank == 0 and args.log:
             print(f"update {update}/{num_updates} step {global_step} SPS {sps} rollout {t_roll:.2f}s "
                   f"update {t_upd:.2f}s return {rec['mean_return']:.3f} kl {rec['approx_kl']:.4f}", flush=True)
+        if on_update is not None and on_update(rec, agent):
+            break
 
     if rank == 0 and args.log:
         os.makedirs(f"{args.save_path}/{run_name}", exist_ok=True)

@@ -33,7 +33,7 @@ EXPORTED = ("vss_abi_version", "vss_source_hash", "vss_error_string", "vss_step"
             "vss_reset_dones_replay",
             "vss_compute_observations", "vss_mlp_packed_size", "vss_mlp_pack", "vss_policy_forward",
             "vss_value_forward_masked", "vss_episode_stats", "vss_tanh_grad_chunks", "vss_tanh_grad_bias",
-            "vss_linear_tanh", "vss_linear_tanh_backward_chunks", "vss_linear_tanh_backward",
+            "vss_linear_tanh", "vss_linear_tanh_out", "vss_linear_tanh_backward_chunks", "vss_linear_tanh_backward",
             "vss_output_backward_chunks", "vss_output_backward")
 
 
@@ -140,6 +140,8 @@ def load() -> ctypes.CDLL:
     L.vss_tanh_grad_bias.restype = ctypes.c_int
     L.vss_linear_tanh.argtypes = [P, i64, i32, i32, P, P, P, P]
     L.vss_linear_tanh.restype = ctypes.c_int
+    L.vss_linear_tanh_out.argtypes = [P, i64, i32, i32, P, P, P, P, i32, P, P]
+    L.vss_linear_tanh_out.restype = ctypes.c_int
     L.vss_linear_tanh_backward_chunks.argtypes = [i64, i32, i32]
     L.vss_linear_tanh_backward_chunks.restype = i64
     L.vss_linear_tanh_backward.argtypes = [P, i64, i32, i32, P, P, P, P, P]

@@ -2,6 +2,7 @@
 
     gz, db = tanh_grad_bias(gy, y)                # gz = gy * (1 - y^2), db = gz.sum(0)
     y = linear_tanh(x, w, b)                      # tanh(x @ w.T + b)
+    y, out = linear_tanh_out(x, w, b, w_o, b_o)   # the same plus the output layer y @ w_o.T + b_o
     gz, db = linear_tanh_backward(gz_next, w_next, y)
                                                   # gz = (gz_next @ w_next) * (1 - y^2), db = gz.sum(0)
     gz, db, dw = output_backward(g_out, w_out, y) # the same through the output layer, plus its
@@ -76,6 +77,32 @@ def linear_tanh(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tens
     N.check(lib.vss_linear_tanh(N.stream_of(x.device), rows, k, n, x.data_ptr(), w.data_ptr(), b.data_ptr(),
                                 y.data_ptr()), "vss_linear_tanh")
     return y
+
+
+def linear_tanh_out_ok(rows: int, k: int, n: int, k_out: int) -> bool:
+    """Shapes vss_linear_tanh_out takes (the last hidden layer of the Agent's MLPs at the update's
+    minibatch sizes): n = 256, rows % 256 == 0, k % 64 == 0, k_out in {1, 2, 6}."""
+    return n == 256 and rows > 0 and rows % 256 == 0 and k % 64 == 0 and k_out in (1, 2, 6)
+
+
+def linear_tanh_out(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out: torch.Tensor, b_out: torch.Tensor):
+    """(y, out): y = tanh(x @ w.T + b) and out = y @ w_out.T + b_out (the output nn.Linear) from ONE
+    launch: the output layer's partial sums come from the GEMM's epilogue (vss_linear_tanh_out)."""
+    rows, k = x.shape
+    n, k_out = w.shape[0], w_out.shape[0]
+    if x.device.type != "cuda":
+        y = torch.addmm(b, x, w.t()).tanh_()
+        return y, torch.addmm(b_out, y, w_out.t())
+    if w.shape != (n, k) or b.shape != (n,) or w_out.shape != (k_out, n) or b_out.shape != (k_out,) \
+            or not linear_tanh_out_ok(rows, k, n, k_out):
+        raise ValueError(f"linear_tanh_out: x {tuple(x.shape)}, w {tuple(w.shape)}, w_out {tuple(w_out.shape)}")
+    _fp32_2d("vss_linear_tanh_out", x, w, b, w_out, b_out)
+    x, w, b, w_out = x.contiguous(), w.contiguous(), b.contiguous(), w_out.contiguous()
+    y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
+    part = torch.empty((n // 64, rows, k_out), device=x.device, dtype=torch.float32)
+    N.check(N.load().vss_linear_tanh_out(N.stream_of(x.device), rows, k, n, x.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                         y.data_ptr(), k_out, w_out.data_ptr(), part.data_ptr()), "vss_linear_tanh_out")
+    return y, part.sum(0).add_(b_out)
 
 
 def linear_tanh_backward(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.Tensor):

@@ -239,3 +239,35 @@ def test_update_gradients_through_hip_match_autograd_gpu(rows, mlp, act_dim, mon
     grads = torch.autograd.grad(loss, list(agent.parameters()))
     for (name, _), u, v in zip(agent.named_parameters(), grads, grads_ref):
         torch.testing.assert_close(u, v, rtol=2e-4, atol=2e-4 * float(v.abs().max()) + 1e-6, msg=name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k_out", [1, 2, 6])
+@pytest.mark.parametrize("rows", [256, 2048 + 256])
+def test_linear_tanh_out_matches_linear_tanh_and_addmm_gpu(rows, k_out):
+    """vss_linear_tanh_out (the last hidden layer with the output layer folded into its epilogue,
+    ppo…:104-111): y bit-identical to vss_linear_tanh (same kernel body), the output layer within
+    fp32 summation-order rounding of addmm."""
+    from vss_amd.update import linear_tanh_out
+    g = torch.Generator(device="cuda").manual_seed(rows + k_out)
+    x = torch.randn(rows, 512, device="cuda", generator=g)
+    w = torch.randn(256, 512, device="cuda", generator=g) / 512 ** 0.5
+    b = torch.randn(256, device="cuda", generator=g) * 0.1
+    w_o = torch.randn(k_out, 256, device="cuda", generator=g) / 16
+    b_o = torch.randn(k_out, device="cuda", generator=g)
+    y, out = linear_tanh_out(x, w, b, w_o, b_o)
+    assert torch.equal(y, linear_tanh(x, w, b))
+    want = torch.addmm(b_o, y.double(), w_o.double().t()).float()
+    torch.testing.assert_close(out, want, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_linear_tanh_out_refusals_gpu():
+    lib = N.load()
+    buf = torch.zeros(1 << 20, device="cuda")
+    p, s = buf.data_ptr(), N.stream_of(buf.device)
+    assert lib.vss_linear_tanh_out(s, 200, 512, 256, p, p, p, p, 2, p, p) != 0   # rows % 256
+    assert lib.vss_linear_tanh_out(s, 256, 512, 512, p, p, p, p, 2, p, p) != 0   # n_out != 256
+    assert lib.vss_linear_tanh_out(s, 256, 512, 256, p, p, p, p, 3, p, p) != 0   # k_out
+    assert lib.vss_linear_tanh_out(s, 256, 96, 256, p, p, p, p, 2, p, p) != 0    # k_in % 64
+    assert lib.vss_linear_tanh_out(s, 256, 512, 256, p, p, p, p, 2, p + 4, p) != 0  # misaligned w_out

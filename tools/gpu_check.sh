@@ -46,7 +46,7 @@ case ",$STEPS," in *,pmcl3,*)
   run rocprof_write_l3 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_l3_$TAG" -o run -- \
       python3 bench.py --fields 131072 --steps 20 --warmup 5 --no-cpu-baseline --ppo-updates 0 --l3-check-fields 0 --rollout-k 0 ;;
 esac
-case ",$STEPS," in *,tupd,*) run pytest_update 600 python -m pytest tests/test_update.py tests/test_ppo.py -m gpu -x -q ;; esac
+case ",$STEPS," in *,tupd,*) run pytest_update 600 python -u -m pytest tests/test_update.py tests/test_ppo.py tests/test_policy.py -m gpu -x -v --timeout 200 --timeout-method thread ;; esac
 # the update's fused-epilogue GEMMs: unit tests, kernel bench vs torch, PPO update fused vs split
 case ",$STEPS," in *,gemm,*)
   run pytest_update 500 python -u -m pytest tests/test_update.py -m gpu -x -v --timeout 120 --timeout-method thread
@@ -95,6 +95,15 @@ case ",$STEPS," in *,profall,*)
   run prof_policy 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_policy_$TAG" -o run -- \
       python3 tools/policy_bench.py
   run pmc_policy 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_WAVES SQ_BUSY_CYCLES --output-format csv -d "$OUT/pmc_policy_$TAG" -o run -- \
+      python3 tools/policy_bench.py ;;
+esac
+# the rollout policy kernel: parity tests, timing, MFMA-busy and stall counters (separate passes)
+case ",$STEPS," in *,pol,*)
+  run pytest_policy 300 python -u -m pytest tests/test_policy.py -m gpu -x -v --timeout 120 --timeout-method thread && \
+  run policy_bench 300 python -u tools/policy_bench.py && \
+  run pmc_policy 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_WAVES SQ_BUSY_CYCLES --output-format csv -d "$OUT/pmc_policy_$TAG" -o run -- \
+      python3 tools/policy_bench.py && \
+  run pmc_policy_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU --output-format csv -d "$OUT/pmc_policy_sq_$TAG" -o run -- \
       python3 tools/policy_bench.py ;;
 esac
 echo "session done" | tee -a "$OUT/session.log"

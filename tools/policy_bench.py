@@ -70,6 +70,17 @@ def main():
                                  agent.actor_logstd.data_ptr(), fused._critic.data_ptr(), 1, 1, None,
                                  act.data_ptr(), lp.data_ptr(), None, v.data_ptr(), None)
         var[os.path.basename(path)] = timeit(run)
+    # diagnostic: the same launch with the actor's weights streamed twice (as actor and as "critic"):
+    # a 2.1 MB stream that fits one XCD's 4 MB L2, against the 4.3 MB actor + critic stream
+    act = torch.empty(rows, 2, device="cuda")
+    lp = torch.empty(rows, device="cuda")
+    v = torch.empty(rows, 1, device="cuda")
+    st = N.stream_of(torch.device("cuda"))
+    L0 = N.load()
+    var["actor_weights_twice (diagnostic, wrong values)"] = timeit(lambda: L0.vss_policy_forward(
+        st, rows, 2, obs.data_ptr(), fused._actor.data_ptr(), agent.actor_logstd.data_ptr(), fused._actor.data_ptr(),
+        1, 1, None, act.data_ptr(), lp.data_ptr(), None, v.data_ptr(), None))
+    var["critic_only"] = timeit(lambda: fused.get_value(tobs))
     print(json.dumps({"variants_actor_critic_ms": var}))
     print(json.dumps({"rows": rows, "torch_ms_per_step": t_torch, "fused_ms_per_step": t_fused,
                       "speedup": t_torch / t_fused, "fused_actor_critic_ms": t_ac,

@@ -655,14 +655,15 @@ def train(args, on_update=None):
         for step in range(T):
             global_step += E * world
             obs[step] = next_obs
-            with torch.no_grad(), autocast(args, device):
-                if fused is not None:
-                    action, logprob, _, value = fused.get_action_and_value(next_obs)
-                else:
+            if fused is not None:  # written straight into this step's storage rows
+                action, _, _, _ = fused.get_action_and_value(next_obs, out=(actions[step], logprobs[step],
+                                                                             values[step].view(E, 1)))
+            else:
+                with torch.no_grad(), autocast(args, device):
                     action, logprob, _, value = agent.get_action_and_value(next_obs)
-                values[step] = value.flatten()
-            actions[step] = action.float()
-            logprobs[step] = logprob.float()
+                    values[step] = value.flatten()
+                actions[step] = action.float()
+                logprobs[step] = logprob.float()
             next_obs, rewards[step], next_done, info = envs.step(action)
             next_dones[step] = next_done
             next_timeouts[step] = info["time_outs"]

@@ -57,24 +57,30 @@ class FusedPolicy:
         self._pack(self.agent.actor_mean, self.n_act, self._actor)
         self._pack(self.agent.critic, 1, self._critic)
 
-    def _run(self, obs, actor: bool, action=None):
+    def _run(self, obs, actor: bool, action=None, out=None, want_mean=False):
         obs = obs.reshape(-1, 52)
         if obs.dtype != torch.float32 or not obs.is_contiguous() or obs.device != self.device:
             obs = obs.to(self.device, torch.float32).contiguous()
         rows = obs.shape[0]
         dev = self.device
-        value = torch.empty((rows, 1), device=dev)
-        outs = [None] * 4
-        if actor:
-            act_out = torch.empty((rows, self.n_act), device=dev) if action is None else None
-            logp = torch.empty(rows, device=dev)
-            ent = torch.empty(rows, device=dev)
-            mean = torch.empty((rows, self.n_act), device=dev)
-            if action is not None:
-                action = action.to(dev, torch.float32).contiguous()
-                if action.numel() != rows * self.n_act:
-                    raise ValueError(f"action must have {rows} x {self.n_act} elements, got {tuple(action.shape)}")
-            outs = [act_out, logp, ent, mean]
+        if out is not None:
+            # caller-owned outputs (the rollout storage rows): action, log-prob and value written in place
+            act_out, logp, value = out
+            for t, w in ((act_out, rows * self.n_act), (logp, rows), (value, rows)):
+                if t.numel() != w or t.dtype != torch.float32 or t.device != dev or not t.is_contiguous():
+                    raise ValueError("out buffers must be contiguous fp32 on the policy's device with one row per obs")
+            outs = [act_out if action is None else None, logp, None, None]
+        else:
+            value = torch.empty((rows, 1), device=dev)
+            outs = [None] * 4
+            if actor:
+                outs = [torch.empty((rows, self.n_act), device=dev) if action is None else None,
+                        torch.empty(rows, device=dev), torch.empty(rows, device=dev),
+                        torch.empty((rows, self.n_act), device=dev) if want_mean else None]
+        if actor and action is not None:
+            action = action.to(dev, torch.float32).contiguous()
+            if action.numel() != rows * self.n_act:
+                raise ValueError(f"action must have {rows} x {self.n_act} elements, got {tuple(action.shape)}")
         self.counter += 1
         rc = N.load().vss_policy_forward(
             N.stream_of(dev), rows, self.n_act, obs.data_ptr(), self._actor.data_ptr() if actor else None,
@@ -86,8 +92,11 @@ class FusedPolicy:
         return value
 
     @torch.no_grad()
-    def get_action_and_value(self, obs, action=None):
-        a, logp, ent, value, _ = self._run(obs, True, action)
+    def get_action_and_value(self, obs, action=None, out=None):
+        """Agent.get_action_and_value.  out = (action, logprob, value) buffers to write in place (the
+        rollout storage rows; the entropy, which the rollout does not use, is then not computed and
+        returned as None)."""
+        a, logp, ent, value, _ = self._run(obs, True, action, out)
         return a, logp, ent, value
 
     @torch.no_grad()
@@ -112,4 +121,4 @@ class FusedPolicy:
 
     @torch.no_grad()
     def actor_mean(self, obs):
-        return self._run(obs, True)[4]
+        return self._run(obs, True, want_mean=True)[4]

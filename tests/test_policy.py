@@ -120,3 +120,28 @@ def test_rejects_bad_shapes_before_launch():
     out = torch.zeros(64, 1, device=DEV)
     fused.get_value_masked(obs, mask.bool(), out)  # a bool mask (the env's dones) is accepted
     assert torch.equal(out, fused.get_value(obs))
+
+
+def test_outputs_written_into_caller_buffers():
+    """The rollout form (ppo…:262-266 into the storage rows): out=(action, logprob, value) buffers are
+    written in place, with the same values as the allocating form; the entropy is not computed."""
+    from vss_amd.policy import FusedPolicy
+    agent = make_agent(2, 8)
+    fused = FusedPolicy(agent, seed=4)
+    obs = torch.randn(4096 + 7, 52, device=DEV)
+    act = torch.randn(obs.shape[0], 2, device=DEV) * 0.5
+    store_a = torch.zeros((3, obs.shape[0], 2), device=DEV)
+    store_lp = torch.zeros((3, obs.shape[0]), device=DEV)
+    store_v = torch.zeros((3, obs.shape[0]), device=DEV)
+    a, lp, ent, v = fused.get_action_and_value(obs, act, out=(store_a[1], store_lp[1], store_v[1].view(-1, 1)))
+    assert ent is None and lp.data_ptr() == store_lp[1].data_ptr() and v.data_ptr() == store_v[1].data_ptr()
+    _, lp2, _, v2 = fused.get_action_and_value(obs, act)
+    assert torch.equal(store_lp[1], lp2) and torch.equal(store_v[1], v2.view(-1))
+    assert torch.all(store_lp[0] == 0) and torch.all(store_lp[2] == 0)
+    a3, _, _, _ = fused.get_action_and_value(obs, out=(store_a[2], store_lp[2], store_v[2].view(-1, 1)))
+    assert a3.data_ptr() == store_a[2].data_ptr() and not torch.all(store_a[2] == 0)
+    with torch.no_grad():
+        _, lp_t, _, _ = agent.get_action_and_value(obs, store_a[2])
+    torch.testing.assert_close(store_lp[2], lp_t, rtol=2e-5, atol=2e-5)
+    with pytest.raises(ValueError):
+        fused.get_action_and_value(obs, out=(store_a[2], store_lp[2][:-1], store_v[2].view(-1, 1)))

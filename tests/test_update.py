@@ -257,7 +257,7 @@ def test_linear_tanh_out_matches_linear_tanh_and_addmm_gpu(rows, k_out):
     b_o = torch.randn(k_out, device="cuda", generator=g)
     y, out = linear_tanh_out(x, w, b, w_o, b_o)
     assert torch.equal(y, linear_tanh(x, w, b))
-    want = torch.addmm(b_o, y.double(), w_o.double().t()).float()
+    want = torch.addmm(b_o.double(), y.double(), w_o.double().t()).float()
     torch.testing.assert_close(out, want, rtol=1e-5, atol=1e-5)
 
 

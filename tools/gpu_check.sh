@@ -106,4 +106,9 @@ case ",$STEPS," in *,pol,*)
   run pmc_policy_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU --output-format csv -d "$OUT/pmc_policy_sq_$TAG" -o run -- \
       python3 tools/policy_bench.py ;;
 esac
+# wall-clock to a trained policy (score >= 0.9 vs the zero team) at the reference's defaults
+case ",$STEPS," in *,tts,*)
+  run tts_sa_4095 900 python -u tools/time_to_score.py --env-id sa --num-envs 4095 --eval-every 10 --max-steps 3e8 ;; esac
+case ",$STEPS," in *,tts65k,*)
+  run tts_sa_65536 1100 python -u tools/time_to_score.py --env-id sa --num-envs 65536 --eval-every 8 --max-steps 1.6e9 ;; esac
 echo "session done" | tee -a "$OUT/session.log"

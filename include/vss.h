@@ -316,6 +316,38 @@ int vss_output_backward(void* stream, int64_t rows, int32_t k_pad, int32_t n, co
                         const float* y, float* grad_in, float* bias_partial, float* wgrad_partial);
 
 /* ---------------------------------------------------------------------------------------------
+ * The update's hidden-layer GEMMs in fp32 arithmetic on the bf16 matrix cores (csrc/vss_gemm_x6.hip;
+ * ppo_continuous_action_isaacgym.py:104-111 under the update's forward ppo…:331 and loss.backward()
+ * ppo…:357).  Every fp32 operand is split exactly into three bf16 parts (hi + mid + lo) and each
+ * product is the six partial products above 2^-23 |a||b|, accumulated in fp32: the error is that of
+ * an fp32 GEMM (tests/test_gemm_x6.py).  Exact shapes only (the update's minibatches); VSS_E_ARG
+ * otherwise, and the caller uses the fp32-MFMA entries above.
+ *
+ * vss_linear_tanh_bf16x6 / _out_bf16x6 / vss_linear_tanh_backward_bf16x6: the same contracts as
+ * vss_linear_tanh / vss_linear_tanh_out / vss_linear_tanh_backward with rows % 256 == 0,
+ * n_out % 128 == 0, k % 64 == 0 (k_in resp. k_next); the backward's bias gradient is the sum over the
+ * vss_linear_tanh_backward_chunks_bf16x6 parts.
+ *
+ * vss_weight_grad_bf16x6: a Linear layer's weight gradient (autograd of nn.Linear, ppo…:357)
+ *   partial[s][o][i] = sum over the rows r of part s of grad[r][o] x[r][i]
+ * grad (rows, n_out) = the layer's output gradient, x (rows, k_in) = its input; dW = the sum over the
+ * vss_weight_grad_chunks_bf16x6(rows, n_out, k_in) parts (-1 for a bad shape).  rows % 64 == 0,
+ * n_out % 256 == 0, k_in % 128 == 0; every pointer 16-B aligned.  Replaces hipBLASLt's split-K
+ * grad^T x GEMM.
+ * ------------------------------------------------------------------------------------------- */
+int vss_linear_tanh_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
+                           const float* bias, float* y);
+int vss_linear_tanh_out_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x,
+                               const float* w, const float* bias, float* y, int32_t k_out, const float* w_out,
+                               float* out_part);
+int64_t vss_linear_tanh_backward_chunks_bf16x6(int64_t rows, int32_t k_next, int32_t n_out);
+int vss_linear_tanh_backward_bf16x6(void* stream, int64_t rows, int32_t k_next, int32_t n_out, const float* grad_next,
+                                    const float* w_next_t, const float* y, float* grad_in, float* bias_partial);
+int64_t vss_weight_grad_chunks_bf16x6(int64_t rows, int32_t n_out, int32_t k_in);
+int vss_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_in, const float* grad, const float* x,
+                           float* partial);
+
+/* ---------------------------------------------------------------------------------------------
  * Episode statistics: RecordEpisodeStatisticsTorch.step (envs/wrappers.py:66-87)
  * for `rows` learner rows in one launch, in the reference's order:
  *   ep_returns += rews; ep_lengths += 1; returned_returns = ep_returns; returned_lengths =

@@ -1,0 +1,544 @@
+// vss_gemm_x6.hip — the PPO update's GEMMs in fp32 arithmetic on the bf16 matrix cores (gfx950).
+//
+// SURVEY §8 A13 (ppo_continuous_action_isaacgym.py:306-353): one update back-propagates 32 minibatches
+// of 2,097,152 rows through both 5-layer MLPs (ppo…:104-125), 4.3e14 FLOP, 94 % of it in the hidden
+// layers' GEMMs.  gfx950's fp32-input MFMA (v_mfma_f32_32x32x2_f32, vss_update.hip) peaks at 157 TF;
+// its bf16 MFMA at 16x that.  This file computes the same fp32 products on the bf16 pipe:
+//
+//   every fp32 operand is split EXACTLY into three bf16 parts, v = hi + mid + lo:
+//     hi  = bf16_rne(v),  r1 = v - hi          (exact in fp32: r1 has <= 16 significant bits)
+//     mid = bf16_rne(r1), lo = r1 - mid        (exact: lo has <= 8 significant bits, a bf16)
+//   so |mid| <= 2^-8 |v|, |lo| <= 2^-16 |v| (relative to v's exponent), and
+//     a b = ah bh + (ah bm + am bh) + (ah bl + am bm + al bh) + [am bl + al bm + al bl]
+//   The six products before the bracket are bf16 x bf16 products (exact in the fp32 accumulator);
+//   the bracket is below 2^-23 |a||b| (about one fp32 ulp of the product) and is dropped.  Each K step
+//   of 32 runs the six products as six v_mfma_f32_16x16x32_bf16, smallest first, into one fp32
+//   accumulator.  Error vs an fp64 reference: that of an fp32 GEMM (tests/test_gemm_x6.py measures it
+//   beside the fp32 MFMA kernels and hipBLASLt's fp32 GEMM).
+//
+// Orientation: the kernel computes D[i][j] = sum_t P[i][t] Q[j][t] and stores D transposed,
+// out[j][i] (i contiguous): an accumulator of v_mfma_f32_16x16x32_bf16 holds rows 4 (lane >> 4) ..
+// +3 of column lane & 15, i.e. four consecutive i of one j, one 16-B store.
+//   forward   (vss_linear_tanh_bf16x6):          i = output feature (P = W, (n, k)), j = row (Q = x)
+//   backward  (vss_linear_tanh_backward_bf16x6): i = feature (P = W_next^T, (n, k_next)), j = row (Q = grad_next)
+//   weight gradient (vss_weight_grad_bf16x6):     i = input feature (P = x^T), j = output feature
+//                                                 (Q = grad^T), contraction over the rows, split in S parts
+// P and Q are staged from global memory through registers (fp32), split, and written into a
+// double-buffered LDS image [plane][k group of 8][row][8 bf16] (group stride padded by 64 B: the
+// staging writes and the fragment reads are conflict-free).  "Row" operands (forward / backward) are
+// K-contiguous in global memory (2 x 16-B loads per 8-wide group); "transposed" operands (weight
+// gradient) have the contraction as their ROW index in global memory, and each lane gathers a group
+// of 8 rows of one column (8 dword loads, each 256 B contiguous across the wave).
+//
+// Block: BI x BJ = 128 x 256 outputs, 8 waves as 2 (i) x 4 (j), each 64 x 64 = 4 x 4 MFMA tiles; one
+// block per CU (147 KB LDS), persistent over the work items with one flat K pipeline (two register
+// sets: a K tile's loads are issued two MFMA phases before the LDS write that consumes them), and the
+// XCD-aware slot map of vss_update.hip (the i tiles of a row band run together on one XCD).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/vss.h"
+
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "vss_gemm_x6.hip targets gfx950 (CDNA4) only: v_mfma_f32_16x16x32_bf16, v_cvt_pk_bf16_f32"
+#endif
+
+namespace vx6 {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+enum { EPI_TANH = 0, EPI_DTANH = 1, EPI_TANH_OUT = 2, EPI_WGRAD = 3 };
+enum { ST_ROW = 0, ST_TR = 1 };
+
+constexpr int KT = 32;  // K tile = one v_mfma_f32_16x16x32_bf16 step
+
+// tanh as vss_update.hip's tanh_f32 (odd polynomial below 0.3, exp2 form above)
+__device__ __forceinline__ float tanh_f32(float z) {
+  const float a = fabsf(z), s = z * z;
+  const float poly = z + z * s * (-0.333333343f + s * (0.133333340f + s * (-0.0539682545f + s * 0.0218694885f)));
+  const float t = __builtin_amdgcn_exp2f(-2.8853900817779268f * a);
+  const float ex = copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), z);
+  return a < 0.3f ? poly : ex;
+}
+
+// two floats -> packed bf16 (round to nearest even, v_cvt_pk_bf16_f32), element 0 in the low half
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  const bf16x2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+// the exact three-way split of 8 floats (one k group) into hi / mid / lo bf16x8
+__device__ __forceinline__ void split8(const float (&v)[8], u32x4& hi, u32x4& mid, u32x4& lo) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float a = v[2 * p], b = v[2 * p + 1];
+    const uint32_t h = pk_bf16(a, b);
+    const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xFFFF0000u);
+    const uint32_t m = pk_bf16(ra, rb);
+    const float sa = ra - __uint_as_float(m << 16), sb = rb - __uint_as_float(m & 0xFFFF0000u);
+    // sa, sb have <= 8 significant bits: their upper halves are exact bf16
+    const uint32_t l = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
+    hi[p] = h;
+    mid[p] = m;
+    lo[p] = l;
+  }
+}
+
+// LDS image of an R-row operand tile for one K tile: [plane 3][group 4][R][8 bf16]; 16 B per (row,
+// group), group stride R * 16 + 64 B (so the 16 lanes of a staging write pass -- 4 rows x 4 groups --
+// and of a fragment read -- 16 rows of one group -- hit 64 distinct banks)
+template <int R>
+struct Img {
+  static constexpr int GS = R * 16 + 64;  // bytes
+  static constexpr int PS = 4 * GS;
+  static constexpr int BYTES = 3 * PS;
+};
+
+template <int BI_, int BJ_, int WI_, int WJ_>
+struct Cfg {
+  static constexpr int BI = BI_, BJ = BJ_, WI = WI_, WJ = WJ_;
+  static constexpr int THREADS = 64 * WI * WJ;
+  static constexpr int WTI = BI / WI, WTJ = BJ / WJ;  // one wave's output extent
+  static constexpr int TI = WTI / 16, TJ = WTJ / 16;  // MFMA tiles per wave
+  static constexpr int PI = BI * 4 / THREADS, PJ = BJ * 4 / THREADS;  // (row, group) pairs per thread
+  static constexpr int BUF = Img<BI>::BYTES + Img<BJ>::BYTES;
+  static constexpr int LDS = 2 * BUF;
+  static_assert(PI * THREADS == BI * 4 && PJ * THREADS == BJ * 4, "staging pairs must tile the block");
+  static_assert(WTI == 64, "a wave's i extent is one 64-feature slice (EPI_TANH_OUT)");
+  static_assert(LDS <= 160 * 1024, "one block per CU");
+};
+using CfgA = Cfg<128, 256, 2, 4>;
+
+struct Args {
+  int32_t ni, nj;          // i tiles, j tiles (of BI, BJ)
+  int32_t ktiles;          // K tiles per work item (even)
+  int32_t items;           // work items = ni * nj * splits
+  int32_t splits;          // EPI_WGRAD: contraction parts
+  int64_t ldp, ldq;        // row strides (floats) of P and Q in global memory
+  const float* p;          // ST_ROW: (I, K) rows; ST_TR: (K, I), i.e. rows of the contraction
+  const float* q;          // ST_ROW: (J, K);      ST_TR: (K, J)
+  int64_t ldo;             // output row stride (floats): out[j][i]
+  float* out;              // (J, I) (EPI_WGRAD: (splits, J, I))
+  const float* bias;       // EPI_TANH*: (I)
+  const float* y;          // EPI_DTANH: (J, I) the tanh output the gradient passes through
+  float* partial;          // EPI_DTANH: (grid / ni, I) column sums of out
+  const float* w_out;      // EPI_TANH_OUT: (KO, I)
+  float* out_part;         // EPI_TANH_OUT: (I / 64, J, KO)
+};
+
+// one thread's raw fp32 operands of one K tile: PI + PJ groups of 8
+template <class C>
+struct Stage {
+  f32x4 v[C::PI + C::PJ][2];
+};
+
+template <int MODE, int R, int NP, class C>
+__device__ __forceinline__ void load_op(f32x4 (*dst)[2], const float* base, int64_t ld, int64_t k0) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {
+    const int pr = t + C::THREADS * u;
+    if constexpr (MODE == ST_ROW) {
+      const int g = pr & 3, row = pr >> 2;
+      const float* src = base + (int64_t)row * ld + k0 + 8 * g;
+      dst[u][0] = *reinterpret_cast<const f32x4*>(src);
+      dst[u][1] = *reinterpret_cast<const f32x4*>(src + 4);
+    } else {
+      const int row = pr % R, g = pr / R;
+      const float* src = base + (k0 + 8 * g) * ld + row;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dst[u][e >> 2][e & 3] = src[e * ld];
+    }
+  }
+}
+
+template <int MODE, int R, int NP, class C>
+__device__ __forceinline__ void write_op(const f32x4 (*src)[2], char* img) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {
+    const int pr = t + C::THREADS * u;
+    int g, row;
+    if constexpr (MODE == ST_ROW) {
+      g = pr & 3;
+      row = pr >> 2;
+    } else {
+      row = pr % R;
+      g = pr / R;
+    }
+    const float v[8] = {src[u][0][0], src[u][0][1], src[u][0][2], src[u][0][3],
+                        src[u][1][0], src[u][1][1], src[u][1][2], src[u][1][3]};
+    u32x4 hi, mid, lo;
+    split8(v, hi, mid, lo);
+    char* d = img + g * Img<R>::GS + row * 16;
+    *reinterpret_cast<u32x4*>(d) = hi;
+    *reinterpret_cast<u32x4*>(d + Img<R>::PS) = mid;
+    *reinterpret_cast<u32x4*>(d + 2 * Img<R>::PS) = lo;
+  }
+}
+
+// sum over the 16 lanes of a DPP row (as vss_update.hip row16_sum)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f32<0xB1>(v);
+  v += dpp_f32<0x4E>(v);
+  v += dpp_f32<0x141>(v);
+  v += dpp_f32<0x140>(v);
+  return v;
+}
+
+template <int EPI, int SP, int SQ, class C, int KO = 0>
+__global__ __launch_bounds__(C::THREADS, 1) void gemm_x6_kernel(Args a) {
+  constexpr int BI = C::BI, BJ = C::BJ, TI = C::TI, TJ = C::TJ, PI = C::PI, PJ = C::PJ;
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS];
+  __shared__ float epi_lds[EPI == EPI_TANH_OUT ? KO * 256 + BI : (EPI == EPI_WGRAD ? 1 : BI)];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wi = wv / C::WJ, wj = wv % C::WJ;
+  const int G = gridDim.x;
+  const int slot = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  if (slot >= a.items) return;
+  const int per_split = a.ni * a.nj;
+
+  // work item w -> (split, j tile, i tile); j-band major so the ni i tiles of a band are consecutive
+  auto item_ij = [&](int w, int& it, int& jt, int& sp) {
+    sp = w / per_split;
+    const int r = w % per_split;
+    jt = r / a.ni;
+    it = r % a.ni;
+  };
+
+  // per-block constants of a fixed i tile (the host makes G a multiple of 8 ni for EPI != EPI_WGRAD)
+  int it0, jt0, sp0;
+  item_ij(slot, it0, jt0, sp0);
+  if constexpr (EPI != EPI_WGRAD) {
+    for (int i = tid; i < BI; i += C::THREADS) epi_lds[i] = EPI == EPI_DTANH ? 0.f : a.bias[it0 * BI + i];
+    if constexpr (EPI == EPI_TANH_OUT)
+      for (int i = tid; i < KO * 256; i += C::THREADS) epi_lds[BI + i] = a.w_out[i];
+  }
+
+  // fetch cursor over the flat sequence of (item, k tile)
+  int f_item = slot, f_kt = 0;
+  const float* fp;
+  const float* fq;
+  int64_t fk0 = 0;  // contraction offset of the item (EPI_WGRAD split)
+  auto point = [&](int w) {
+    int it, jt, sp;
+    item_ij(w, it, jt, sp);
+    fk0 = (int64_t)sp * a.ktiles * KT;
+    if constexpr (SP == ST_ROW) fp = a.p + (int64_t)it * BI * a.ldp;
+    else fp = a.p + (int64_t)it * BI;
+    if constexpr (SQ == ST_ROW) fq = a.q + (int64_t)jt * BJ * a.ldq;
+    else fq = a.q + (int64_t)jt * BJ;
+  };
+  point(f_item);
+  auto gload = [&](Stage<C>& s) {
+    const int64_t k0 = fk0 + (int64_t)f_kt * KT;
+    load_op<SP, BI, PI, C>(s.v, fp, a.ldp, k0);
+    load_op<SQ, BJ, PJ, C>(s.v + PI, fq, a.ldq, k0);
+    if (++f_kt >= a.ktiles) {
+      if (f_item + G < a.items) {
+        f_kt = 0;
+        f_item += G;
+        point(f_item);
+      } else {
+        f_kt = a.ktiles - 1;  // past the last item: re-load its last K tile (in bounds, never used)
+      }
+    }
+  };
+  auto swrite = [&](const Stage<C>& s, int buf) {
+    char* base = lds + buf * C::BUF;
+    write_op<SP, BI, PI, C>(s.v, base);
+    write_op<SQ, BJ, PJ, C>(s.v + PI, base + Img<BI>::BYTES);
+  };
+
+  f32x4 acc[TI][TJ];
+  const int fr = lane & 15, fg = lane >> 4;  // fragment row, k group
+  auto mfma_tile = [&](int buf) {
+    const char* pb = lds + buf * C::BUF + fg * Img<BI>::GS + (wi * C::WTI + fr) * 16;
+    const char* qb = lds + buf * C::BUF + Img<BI>::BYTES + fg * Img<BJ>::GS + (wj * C::WTJ + fr) * 16;
+    u32x4 pf[3][TI], qf[3][TJ];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) pf[pl][i] = *reinterpret_cast<const u32x4*>(pb + pl * Img<BI>::PS + i * 256);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) qf[pl][j] = *reinterpret_cast<const u32x4*>(qb + pl * Img<BJ>::PS + j * 256);
+    }
+    // the six products, smallest first: lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi
+    constexpr int PP[6] = {2, 0, 1, 1, 0, 0};
+    constexpr int QP[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+    for (int x = 0; x < 6; ++x)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pf[PP[x]][i]),
+                                                              __builtin_bit_cast(bf16x8, qf[QP[x]][j]), acc[i][j], 0, 0, 0);
+  };
+
+  // EPI_DTANH: this lane's column sums, features wi*64 + 16 i + 4 fg + r, over all its tiles
+  float csum[EPI == EPI_DTANH ? TI : 1][4];
+#pragma unroll
+  for (int i = 0; i < (EPI == EPI_DTANH ? TI : 1); ++i) csum[i][0] = csum[i][1] = csum[i][2] = csum[i][3] = 0.f;
+
+  Stage<C> r0, r1;
+  gload(r0);  // K tile 0
+  swrite(r0, 0);
+  gload(r1);  // K tile 1
+  gload(r0);  // K tile 2
+  __syncthreads();
+  int w = slot;
+  for (;;) {
+    const int next = w + G;
+    const bool has_next = next < a.items;
+    int it, jt, sp;
+    item_ij(w, it, jt, sp);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < a.ktiles; kt += 2) {
+      mfma_tile(0);
+      swrite(r1, 1);
+      __syncthreads();
+      gload(r1);
+      mfma_tile(1);
+      swrite(r0, 0);
+      __syncthreads();
+      gload(r0);
+    }
+
+    // epilogue straight from the accumulators: lane holds out[j][i .. i + 3] for
+    // i = i0 + 16 ti + 4 fg, j = j0 + 16 tj + fr
+    const int ib = it * BI + wi * C::WTI, jb = jt * BJ + wj * C::WTJ;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int64_t jg = (int64_t)jb + 16 * j + fr;
+      float od[KO > 0 ? KO : 1];  // EPI_TANH_OUT: this row's output-layer sums over the wave's features
+#pragma unroll
+      for (int o = 0; o < (KO > 0 ? KO : 1); ++o) od[o] = 0.f;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int il = wi * C::WTI + 16 * i + 4 * fg;  // feature within the block's i tile
+        const int ig = it * BI + il;
+        f32x4 v = acc[i][j];
+        if constexpr (EPI == EPI_TANH || EPI == EPI_TANH_OUT) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = tanh_f32(v[r] + epi_lds[il + r]);
+          *reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig) = v;
+          if constexpr (EPI == EPI_TANH_OUT) {
+#pragma unroll
+            for (int o = 0; o < KO; ++o) {
+              const float* wo = epi_lds + BI + o * 256 + ig;
+              float d = v[0] * wo[0];
+              d = fmaf(v[1], wo[1], d);
+              d = fmaf(v[2], wo[2], d);
+              d = fmaf(v[3], wo[3], d);
+              od[o] += d;
+            }
+          }
+        } else if constexpr (EPI == EPI_DTANH) {
+          const f32x4 yv = *reinterpret_cast<const f32x4*>(a.y + jg * a.ldo + ig);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = v[r] * fmaf(-yv[r], yv[r], 1.0f);
+            csum[i][r] += v[r];
+          }
+          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig));
+        } else {  // EPI_WGRAD: the split's partial
+          *reinterpret_cast<f32x4*>(a.out + ((int64_t)sp * a.nj * BJ + jg) * a.ldo + ig) = v;
+        }
+      }
+      if constexpr (EPI == EPI_TANH_OUT) {
+        // the wave's 64-feature slice of the output layer for row jg: the 4 k groups' lanes
+#pragma unroll
+        for (int o = 0; o < KO; ++o) {
+          float d = od[o];
+          d += __shfl_xor(d, 16);
+          d += __shfl_xor(d, 32);
+          if (fg == 0) a.out_part[(((int64_t)ib >> 6) * (a.nj * BJ) + jg) * KO + o] = d;
+        }
+      }
+    }
+    if (!has_next) break;
+    w = next;
+  }
+
+  if constexpr (EPI == EPI_DTANH) {
+    // column sums: the 16 lanes (rows) of each k group, then the WJ waves of a feature slice in a
+    // fixed order (deterministic); partial[slot / ni][feature]
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);  // (WJ, BI)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float s = row16_sum(csum[i][r]);
+        if (fr == 0) red[wj * BI + wi * C::WTI + 16 * i + 4 * fg + r] = s;
+      }
+    __syncthreads();
+    for (int f = tid; f < BI; f += C::THREADS) {
+      float s = red[f];
+#pragma unroll
+      for (int m = 1; m < C::WJ; ++m) s += red[m * BI + f];
+      a.partial[(int64_t)(slot / a.ni) * (a.ni * BI) + it0 * BI + f] = s;
+    }
+  }
+}
+
+constexpr int kGridCus = 256;  // persistent grid sized for MI355X on every device (fixed partial layout)
+
+struct Plan {
+  int32_t ni, nj, ktiles, splits, items, grid;
+};
+
+// forward / backward: exact shapes only (the update's minibatches): rows % 256, n % 128, k % 64
+static bool fb_shape_ok(int64_t rows, int32_t k, int32_t n) {
+  return rows > 0 && rows % CfgA::BJ == 0 && rows / CfgA::BJ <= (1 << 22) && n > 0 && n % CfgA::BI == 0 && n <= 4096 &&
+         k > 0 && k % (2 * KT) == 0 && k <= 65536 && (rows / CfgA::BJ) * (n / CfgA::BI) <= 0x3fffffff;
+}
+
+static Plan fb_plan(int64_t rows, int32_t k, int32_t n) {
+  Plan p;
+  p.ni = n / CfgA::BI;
+  p.nj = (int32_t)(rows / CfgA::BJ);
+  p.ktiles = k / KT;
+  p.splits = 1;
+  p.items = p.ni * p.nj;
+  int g = kGridCus;
+  g -= g % (8 * p.ni);  // a fixed i tile per block, 8 XCD slots
+  p.grid = (g > 0 && g < p.items) ? g : p.items;
+  return p;
+}
+
+// weight gradient: dW (n_out, k_in) = grad^T x over `rows`: k_in % 128, n_out % 256, rows % 64;
+// splits S | rows / 64 so that the ni * nj * S items fill the persistent grid
+static bool wg_shape_ok(int64_t rows, int32_t n_out, int32_t k_in) {
+  return rows > 0 && rows % (2 * KT) == 0 && rows <= (int64_t(1) << 40) && k_in > 0 && k_in % CfgA::BI == 0 &&
+         k_in <= 4096 && n_out > 0 && n_out % CfgA::BJ == 0 && n_out <= 4096;
+}
+
+static Plan wg_plan(int64_t rows, int32_t n_out, int32_t k_in) {
+  Plan p;
+  p.ni = k_in / CfgA::BI;
+  p.nj = n_out / CfgA::BJ;
+  const int64_t pairs = rows / (2 * KT);  // K-tile pairs
+  const int tiles = p.ni * p.nj;
+  int s = kGridCus / tiles;
+  if (s < 1) s = 1;
+  while (s > 1 && pairs % s) --s;  // the largest S <= grid / tiles dividing the K-tile pairs
+  p.splits = s;
+  p.ktiles = (int32_t)(pairs / s * 2);
+  p.items = tiles * s;
+  p.grid = p.items < kGridCus ? p.items : kGridCus;
+  p.grid -= (p.grid % 8 && p.grid > 8) ? p.grid % 8 : 0;
+  return p;
+}
+
+template <int EPI, int SP, int SQ, int KO = 0>
+static int launch(void* stream, Args a, const Plan& pl) {
+  a.ni = pl.ni;
+  a.nj = pl.nj;
+  a.ktiles = pl.ktiles;
+  a.items = pl.items;
+  a.splits = pl.splits;
+  hipLaunchKernelGGL((gemm_x6_kernel<EPI, SP, SQ, CfgA, KO>), dim3((unsigned)pl.grid), dim3(CfgA::THREADS), 0,
+                     (hipStream_t)stream, a);
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+}
+
+static bool misaligned(const void* p) { return !p || (reinterpret_cast<uintptr_t>(p) & 15) != 0; }
+
+}  // namespace vx6
+
+extern "C" {
+
+int vss_linear_tanh_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
+                           const float* bias, float* y) {
+  using namespace vx6;
+  if (!fb_shape_ok(rows, k_in, n_out) || misaligned(x) || misaligned(w) || misaligned(y) || !bias) return VSS_E_ARG;
+  Args a{};
+  a.ldp = k_in;
+  a.ldq = k_in;
+  a.p = w;
+  a.q = x;
+  a.ldo = n_out;
+  a.out = y;
+  a.bias = bias;
+  return launch<EPI_TANH, ST_ROW, ST_ROW>(stream, a, fb_plan(rows, k_in, n_out));
+}
+
+int vss_linear_tanh_out_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
+                               const float* bias, float* y, int32_t k_out, const float* w_out, float* out_part) {
+  using namespace vx6;
+  if (!fb_shape_ok(rows, k_in, n_out) || n_out != 256 || misaligned(x) || misaligned(w) || misaligned(y) || !bias ||
+      !w_out || !out_part || !(k_out == 1 || k_out == 2 || k_out == 6))
+    return VSS_E_ARG;
+  Args a{};
+  a.ldp = k_in;
+  a.ldq = k_in;
+  a.p = w;
+  a.q = x;
+  a.ldo = n_out;
+  a.out = y;
+  a.bias = bias;
+  a.w_out = w_out;
+  a.out_part = out_part;
+  const Plan pl = fb_plan(rows, k_in, n_out);
+  if (k_out == 1) return launch<EPI_TANH_OUT, ST_ROW, ST_ROW, 1>(stream, a, pl);
+  if (k_out == 2) return launch<EPI_TANH_OUT, ST_ROW, ST_ROW, 2>(stream, a, pl);
+  return launch<EPI_TANH_OUT, ST_ROW, ST_ROW, 6>(stream, a, pl);
+}
+
+int64_t vss_linear_tanh_backward_chunks_bf16x6(int64_t rows, int32_t k_next, int32_t n_out) {
+  using namespace vx6;
+  if (!fb_shape_ok(rows, k_next, n_out)) return -1;
+  const Plan pl = fb_plan(rows, k_next, n_out);
+  return pl.grid / pl.ni;
+}
+
+int vss_linear_tanh_backward_bf16x6(void* stream, int64_t rows, int32_t k_next, int32_t n_out, const float* grad_next,
+                                   const float* w_next_t, const float* y, float* grad_in, float* bias_partial) {
+  using namespace vx6;
+  if (!fb_shape_ok(rows, k_next, n_out) || misaligned(grad_next) || misaligned(w_next_t) || misaligned(y) ||
+      misaligned(grad_in) || misaligned(bias_partial))
+    return VSS_E_ARG;
+  Args a{};
+  a.ldp = k_next;
+  a.ldq = k_next;
+  a.p = w_next_t;
+  a.q = grad_next;
+  a.ldo = n_out;
+  a.out = grad_in;
+  a.y = y;
+  a.partial = bias_partial;
+  return launch<EPI_DTANH, ST_ROW, ST_ROW>(stream, a, fb_plan(rows, k_next, n_out));
+}
+
+int64_t vss_weight_grad_chunks_bf16x6(int64_t rows, int32_t n_out, int32_t k_in) {
+  using namespace vx6;
+  if (!wg_shape_ok(rows, n_out, k_in)) return -1;
+  return wg_plan(rows, n_out, k_in).splits;
+}
+
+int vss_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_in, const float* grad, const float* x,
+                           float* partial) {
+  using namespace vx6;
+  if (!wg_shape_ok(rows, n_out, k_in) || misaligned(grad) || misaligned(x) || misaligned(partial)) return VSS_E_ARG;
+  Args a{};
+  a.ldp = k_in;
+  a.ldq = n_out;
+  a.p = x;
+  a.q = grad;
+  a.ldo = k_in;
+  a.out = partial;
+  return launch<EPI_WGRAD, ST_TR, ST_TR>(stream, a, wg_plan(rows, n_out, k_in));
+}
+
+}  // extern "C"

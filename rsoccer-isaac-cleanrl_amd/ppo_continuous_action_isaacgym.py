@@ -34,8 +34,9 @@ from torch.distributions.normal import Normal
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from envs._gym import Box, ObservationWrapper  # noqa: E402
-from vss_amd.update import (gemm_shape_ok, linear_tanh, linear_tanh_backward, linear_tanh_out,  # noqa: E402
-                            linear_tanh_out_ok, output_backward, output_backward_ok, tanh_grad_bias)
+from vss_amd.update import (gemm_shape_ok, linear_tanh, linear_tanh_backward, linear_tanh_backward_x6,  # noqa: E402
+                            linear_tanh_out, linear_tanh_out_ok, linear_tanh_out_x6, linear_tanh_x6, output_backward,
+                            output_backward_ok, tanh_grad_bias, weight_grad_x6, x6_ok, x6_wgrad_ok)
 
 
 def strtobool(x: str) -> bool:
@@ -205,11 +206,14 @@ class _TanhMLP(torch.autograd.Function):
     def forward(ctx, x, *params):
         ws, bs = params[0::2], params[1::2]
         hs = [x]
+        rows = x.shape[0]
         for w, b in zip(ws[:-2], bs[:-2]):
-            hs.append(linear_tanh(hs[-1], w, b))
-        if x.is_cuda and OUTPUT_FWD and linear_tanh_out_ok(x.shape[0], ws[-2].shape[1], ws[-2].shape[0], ws[-1].shape[0]):
-            # the last hidden layer and the output layer in one launch (vss_linear_tanh_out)
-            h, out = linear_tanh_out(hs[-1], ws[-2], bs[-2], ws[-1], bs[-1])
+            x6 = x.is_cuda and UPDATE_GEMM == "x6" and x6_ok(rows, w.shape[1], w.shape[0])
+            hs.append((linear_tanh_x6 if x6 else linear_tanh)(hs[-1], w, b))
+        if x.is_cuda and OUTPUT_FWD and linear_tanh_out_ok(rows, ws[-2].shape[1], ws[-2].shape[0], ws[-1].shape[0]):
+            # the last hidden layer and the output layer in one launch (vss_linear_tanh_out[_bf16x6])
+            x6 = UPDATE_GEMM == "x6" and x6_ok(rows, ws[-2].shape[1], ws[-2].shape[0])
+            h, out = (linear_tanh_out_x6 if x6 else linear_tanh_out)(hs[-1], ws[-2], bs[-2], ws[-1], bs[-1])
             hs.append(h)
         else:
             hs.append(linear_tanh(hs[-1], ws[-2], bs[-2]))
@@ -232,7 +236,13 @@ class _TanhMLP(torch.autograd.Function):
                 grads[2 * layer + 1] = gb
                 gz, gb, grads[2 * layer] = output_backward(gz, ws[layer], hs[layer])
                 continue
-            grads[2 * layer], grads[2 * layer + 1] = _split_k_wgrad(gz, hs[layer]), gb
+            rows = gz.shape[0]
+            x6 = gz.is_cuda and UPDATE_GEMM == "x6"
+            if x6 and x6_wgrad_ok(rows, gz.shape[1], hs[layer].shape[1]):
+                grads[2 * layer] = weight_grad_x6(gz, hs[layer])
+            else:
+                grads[2 * layer] = _split_k_wgrad(gz, hs[layer])
+            grads[2 * layer + 1] = gb
             if layer == 0:
                 break
             w = ws[layer]
@@ -241,7 +251,10 @@ class _TanhMLP(torch.autograd.Function):
                 # GEMM's contraction granule, so this backward is one fused pass as well
                 pad = 4 - gz.shape[1] % 4
                 gz, w = nn.functional.pad(gz, (0, pad)), nn.functional.pad(w, (0, 0, 0, pad))
-            gz, gb = linear_tanh_backward(gz, w, hs[layer])
+            if x6 and x6_ok(rows, gz.shape[1], hs[layer].shape[1]):
+                gz, gb = linear_tanh_backward_x6(gz, w, hs[layer])
+            else:
+                gz, gb = linear_tanh_backward(gz, w, hs[layer])
         gx = gz.mm(ws[0]) if ctx.needs_input_grad[0] else None
         return (gx, *grads)
 
@@ -251,6 +264,10 @@ class _TanhMLP(torch.autograd.Function):
 # (hipBLASLt GEMMs + the one-pass HIP tanh backward: 3.99 s).  DESIGN.md §5.3 / §7,
 # profiles/r02_gemm_fused_bench.log, profiles/r02_ppo_sa_fused_vs_split_seeds.json.
 UPDATE_MLP = os.environ.get("VSS_UPDATE_MLP", "fused")
+# the fused path's GEMM arithmetic: "x6" (default) = fp32 products on the bf16 matrix cores from an
+# exact 3-way bf16 split of every operand (csrc/vss_gemm_x6.hip; error vs fp64 at or below the fp32
+# GEMMs', tests/test_gemm_x6.py), where the shapes are exact; "fp32" = the fp32-MFMA kernels only
+UPDATE_GEMM = os.environ.get("VSS_UPDATE_GEMM", "x6")
 # the fused path's output layer: "1" (default) = its backward and weight gradient in one streaming
 # pass (vss_output_backward), "0" = the padded backward + a split-K dW GEMM (A/B switch)
 OUTPUT_BWD = os.environ.get("VSS_OUTPUT_BWD", "1") == "1"

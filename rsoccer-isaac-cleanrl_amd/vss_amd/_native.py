@@ -22,7 +22,8 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "vss.h"
 
 # the sources the Makefile stamps into the library, in its order (csrc/Makefile STAMPED)
 STAMPED = (os.path.join(CSRC, "vss_step.hip"), os.path.join(CSRC, "vss_update.hip"),
-           os.path.join(CSRC, "vss_policy.hip"), HEADER, os.path.join(CSRC, "Makefile"))
+           os.path.join(CSRC, "vss_policy.hip"), os.path.join(CSRC, "vss_gemm_x6.hip"), HEADER,
+           os.path.join(CSRC, "Makefile"))
 
 ABI_VERSION = 2
 MODE_FULL, MODE_SA, MODE_CMA, MODE_DMA = 0, 1, 2, 3
@@ -34,7 +35,9 @@ EXPORTED = ("vss_abi_version", "vss_source_hash", "vss_error_string", "vss_step"
             "vss_compute_observations", "vss_mlp_packed_size", "vss_mlp_pack", "vss_policy_forward",
             "vss_value_forward_masked", "vss_episode_stats", "vss_tanh_grad_chunks", "vss_tanh_grad_bias",
             "vss_linear_tanh", "vss_linear_tanh_out", "vss_linear_tanh_backward_chunks", "vss_linear_tanh_backward",
-            "vss_output_backward_chunks", "vss_output_backward")
+            "vss_output_backward_chunks", "vss_output_backward", "vss_linear_tanh_bf16x6",
+            "vss_linear_tanh_out_bf16x6", "vss_linear_tanh_backward_chunks_bf16x6", "vss_linear_tanh_backward_bf16x6",
+            "vss_weight_grad_chunks_bf16x6", "vss_weight_grad_bf16x6")
 
 
 class VssParams(ctypes.Structure):
@@ -150,6 +153,18 @@ def load() -> ctypes.CDLL:
     L.vss_output_backward_chunks.restype = i64
     L.vss_output_backward.argtypes = [P, i64, i32, i32, P, P, P, P, P, P]
     L.vss_output_backward.restype = ctypes.c_int
+    L.vss_linear_tanh_bf16x6.argtypes = [P, i64, i32, i32, P, P, P, P]
+    L.vss_linear_tanh_bf16x6.restype = ctypes.c_int
+    L.vss_linear_tanh_out_bf16x6.argtypes = [P, i64, i32, i32, P, P, P, P, i32, P, P]
+    L.vss_linear_tanh_out_bf16x6.restype = ctypes.c_int
+    L.vss_linear_tanh_backward_chunks_bf16x6.argtypes = [i64, i32, i32]
+    L.vss_linear_tanh_backward_chunks_bf16x6.restype = i64
+    L.vss_linear_tanh_backward_bf16x6.argtypes = [P, i64, i32, i32, P, P, P, P, P]
+    L.vss_linear_tanh_backward_bf16x6.restype = ctypes.c_int
+    L.vss_weight_grad_chunks_bf16x6.argtypes = [i64, i32, i32]
+    L.vss_weight_grad_chunks_bf16x6.restype = i64
+    L.vss_weight_grad_bf16x6.argtypes = [P, i64, i32, i32, P, P, P]
+    L.vss_weight_grad_bf16x6.restype = ctypes.c_int
     if L.vss_abi_version() != ABI_VERSION:
         raise NativeError(f"libvss_amd ABI {L.vss_abi_version()} != expected {ABI_VERSION}")
     _lib = L

@@ -172,3 +172,88 @@ def output_backward(g_out: torch.Tensor, w_out: torch.Tensor, y: torch.Tensor):
                                     y.data_ptr(), gz.data_ptr(), bpart.data_ptr(), wpart.data_ptr()),
             "vss_output_backward")
     return gz, bpart.sum(0), wpart.sum(0)[:k_out]
+
+
+# ---- the same GEMMs in fp32 arithmetic on the bf16 matrix cores (csrc/vss_gemm_x6.hip) ----------------
+# Every operand is split exactly into three bf16 parts and each product is summed from the six partial
+# products above 2^-23 |a||b| in fp32 (tests/test_gemm_x6.py: the error is that of an fp32 GEMM).
+# Exact shapes only; the callers keep the fp32-MFMA entries above for the others.
+
+def x6_ok(rows: int, k: int, n: int) -> bool:
+    """Shapes the bf16x6 forward / backward take: rows % 256, n % 128, k % 64."""
+    return rows > 0 and rows % 256 == 0 and n > 0 and n % 128 == 0 and n <= 4096 and k > 0 and k % 64 == 0
+
+
+def x6_wgrad_ok(rows: int, n_out: int, k_in: int) -> bool:
+    """Shapes the bf16x6 weight gradient takes: rows % 64, n_out % 256, k_in % 128."""
+    return rows > 0 and rows % 64 == 0 and n_out % 256 == 0 and 0 < n_out <= 4096 and k_in % 128 == 0 \
+        and 0 < k_in <= 4096
+
+
+def _x6_check(name, cond, *ts):
+    if not cond:
+        raise ValueError(f"{name}: shape outside the bf16x6 kernels' exact shapes: {[tuple(t.shape) for t in ts]}")
+    _fp32_2d(name, *ts)
+    for t in ts:
+        if t.device.type != "cuda":
+            raise ValueError(f"{name}: ROCm tensors only (no CPU path)")
+
+
+def linear_tanh_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """linear_tanh on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_bf16x6)."""
+    rows, k = x.shape
+    n = w.shape[0]
+    _x6_check("vss_linear_tanh_bf16x6", w.shape == (n, k) and b.shape == (n,) and x6_ok(rows, k, n), x, w, b)
+    x, w, b = x.contiguous(), w.contiguous(), b.contiguous()
+    y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
+    N.check(N.load().vss_linear_tanh_bf16x6(N.stream_of(x.device), rows, k, n, x.data_ptr(), w.data_ptr(),
+                                            b.data_ptr(), y.data_ptr()), "vss_linear_tanh_bf16x6")
+    return y
+
+
+def linear_tanh_out_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out: torch.Tensor, b_out: torch.Tensor):
+    """linear_tanh_out on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_out_bf16x6)."""
+    rows, k = x.shape
+    n, k_out = w.shape[0], w_out.shape[0]
+    _x6_check("vss_linear_tanh_out_bf16x6", w.shape == (n, k) and b.shape == (n,) and w_out.shape == (k_out, n)
+              and b_out.shape == (k_out,) and n == 256 and k_out in (1, 2, 6) and x6_ok(rows, k, n), x, w, b, w_out)
+    x, w, b, w_out = x.contiguous(), w.contiguous(), b.contiguous(), w_out.contiguous()
+    y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
+    part = torch.empty((n // 64, rows, k_out), device=x.device, dtype=torch.float32)
+    N.check(N.load().vss_linear_tanh_out_bf16x6(N.stream_of(x.device), rows, k, n, x.data_ptr(), w.data_ptr(),
+                                                b.data_ptr(), y.data_ptr(), k_out, w_out.data_ptr(), part.data_ptr()),
+            "vss_linear_tanh_out_bf16x6")
+    return y, part.sum(0).add_(b_out)
+
+
+def linear_tanh_backward_x6(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.Tensor):
+    """linear_tanh_backward on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_backward_bf16x6)."""
+    rows, k_next = gz_next.shape
+    n = y.shape[1]
+    _x6_check("vss_linear_tanh_backward_bf16x6", w_next.shape == (k_next, n) and y.shape[0] == rows
+              and x6_ok(rows, k_next, n), gz_next, w_next, y)
+    lib = N.load()
+    gz_next, y = gz_next.contiguous(), y.contiguous()
+    w_t = w_next.t().contiguous()  # (n, k_next): K-contiguous
+    gz = torch.empty((rows, n), device=y.device, dtype=torch.float32)
+    partial = torch.empty((lib.vss_linear_tanh_backward_chunks_bf16x6(rows, k_next, n), n), device=y.device,
+                          dtype=torch.float32)
+    N.check(lib.vss_linear_tanh_backward_bf16x6(N.stream_of(y.device), rows, k_next, n, gz_next.data_ptr(),
+                                                w_t.data_ptr(), y.data_ptr(), gz.data_ptr(), partial.data_ptr()),
+            "vss_linear_tanh_backward_bf16x6")
+    return gz, partial.sum(0)
+
+
+def weight_grad_x6(grad: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dW = grad.T @ x (a Linear layer's weight gradient, grad (rows, n_out), x (rows, k_in)) on the
+    bf16 matrix cores with fp32 arithmetic, split over the rows (vss_weight_grad_bf16x6)."""
+    rows, n_out = grad.shape
+    k_in = x.shape[1]
+    _x6_check("vss_weight_grad_bf16x6", x.shape[0] == rows and x6_wgrad_ok(rows, n_out, k_in), grad, x)
+    lib = N.load()
+    grad, x = grad.contiguous(), x.contiguous()
+    parts = torch.empty((lib.vss_weight_grad_chunks_bf16x6(rows, n_out, k_in), n_out, k_in), device=x.device,
+                        dtype=torch.float32)
+    N.check(lib.vss_weight_grad_bf16x6(N.stream_of(x.device), rows, n_out, k_in, grad.data_ptr(), x.data_ptr(),
+                                       parts.data_ptr()), "vss_weight_grad_bf16x6")
+    return parts.sum(0)

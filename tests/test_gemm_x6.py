@@ -1,0 +1,172 @@
+"""The update's GEMMs in fp32 arithmetic on the bf16 matrix cores (csrc/vss_gemm_x6.hip): every fp32
+operand split exactly into three bf16 parts, the six partial products above 2^-23 |a||b| summed in
+fp32.  Checked against fp64 evaluations of the same functions, beside the fp32 GEMMs they replace
+(hipBLASLt's torch.mm / addmm and the fp32-MFMA kernels of csrc/vss_update.hip): the bar is the
+fp32 GEMM's own error (tolerance in each test), plus exact results where fp32 is exact (integer
+operands) and the per-product bound of the split (one-row outer products)."""
+import pytest
+import torch
+
+from vss_amd import _native as N
+from vss_amd.update import (linear_tanh, linear_tanh_backward, linear_tanh_backward_x6, linear_tanh_out_x6,
+                            linear_tanh_x6, weight_grad_x6, x6_ok, x6_wgrad_ok)
+
+
+def test_x6_shape_predicates_cpu():
+    assert x6_ok(2097152, 512, 256) and x6_ok(256, 256, 512) and x6_ok(256, 64, 128)
+    assert not x6_ok(200, 512, 256) and not x6_ok(256, 52, 256) and not x6_ok(256, 512, 100)
+    assert x6_wgrad_ok(64, 256, 128) and x6_wgrad_ok(2097152, 512, 512)
+    assert not x6_wgrad_ok(100, 256, 128) and not x6_wgrad_ok(64, 128, 128) and not x6_wgrad_ok(64, 256, 52)
+
+
+def test_x6_refuses_cpu_tensors():
+    x = torch.zeros(256, 64)
+    with pytest.raises(ValueError):
+        linear_tanh_x6(x, torch.zeros(128, 64), torch.zeros(128))
+    with pytest.raises(ValueError):
+        weight_grad_x6(torch.zeros(64, 256), torch.zeros(64, 128))
+
+
+def _rel(out, ref64):
+    d = out.double() - ref64
+    return float(d.abs().max() / ref64.abs().max()), float(d.norm() / ref64.norm())
+
+
+def _ops(rows, k, n, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.tanh(torch.randn(rows, k, device="cuda", generator=g))
+    w = torch.randn(n, k, device="cuda", generator=g) / k ** 0.5
+    b = torch.randn(n, device="cuda", generator=g) * 0.1
+    gz = torch.randn(rows, n, device="cuda", generator=g) * 1e-3
+    y_lo = torch.tanh(torch.randn(rows, k, device="cuda", generator=g))
+    return x, w, b, gz, y_lo
+
+
+SHAPES = [(256, 512), (512, 512), (512, 256), (64, 128), (128, 256)]   # (k, n) forward
+BSHAPES = [(256, 512), (512, 512), (512, 256), (128, 256), (256, 128)]  # backward: from n into k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n", SHAPES)
+@pytest.mark.parametrize("rows", [256, 8192])
+def test_x6_forward_error_at_most_fp32_gpu(rows, k, n):
+    """y = tanh(x W^T + b): error vs fp64 no larger than hipBLASLt's fp32 addmm + tanh (x 1.25 slack)
+    and below 4e-6 of max|y| (tolerance)."""
+    x, w, b, _, _ = _ops(rows, k, n, rows + k * n)
+    ref = torch.tanh(x.double() @ w.double().t() + b.double())
+    e6 = _rel(linear_tanh_x6(x, w, b), ref)
+    et = _rel(torch.addmm(b, x, w.t()).tanh_(), ref)
+    assert e6[0] < 4e-6 and e6[1] < 1.25 * et[1] + 1e-8, (e6, et)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n", BSHAPES)
+@pytest.mark.parametrize("rows", [256, 8192])
+def test_x6_backward_error_at_most_fp32_gpu(rows, k, n):
+    """gz = (g W) * (1 - y^2) and its column sums (the bias gradient): error vs fp64 no larger than
+    torch's fp32 mm (x 1.25 slack); the column sums within 1e-5 relative."""
+    x, w, _, gz, y_lo = _ops(rows, k, n, 3 * rows + k + n)
+    ref = (gz.double() @ w.double()) * (1 - y_lo.double() ** 2)
+    g6, db6 = linear_tanh_backward_x6(gz, w, y_lo)
+    e6 = _rel(g6, ref)
+    et = _rel(gz.mm(w) * (1 - y_lo * y_lo), ref)
+    assert e6[0] < 4e-6 and e6[1] < 1.25 * et[1] + 1e-8, (e6, et)
+    torch.testing.assert_close(db6.double(), ref.sum(0), rtol=1e-5, atol=1e-5 * float(ref.sum(0).abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_out,k_in", [(512, 512), (512, 256), (256, 512), (256, 128)])
+@pytest.mark.parametrize("rows", [64, 8192, 65536 + 64])
+def test_x6_weight_grad_error_at_most_fp32_gpu(rows, n_out, k_in):
+    """dW = g^T x over the rows (split in parts): error vs fp64 no larger than torch's fp32 mm."""
+    g = torch.Generator(device="cuda").manual_seed(rows + n_out + k_in)
+    gz = torch.randn(rows, n_out, device="cuda", generator=g) * 1e-3
+    x = torch.tanh(torch.randn(rows, k_in, device="cuda", generator=g))
+    ref = gz.double().t() @ x.double()
+    e6 = _rel(weight_grad_x6(gz, x), ref)
+    et = _rel(gz.t().mm(x), ref)
+    assert e6[0] < 4e-6 and e6[1] < 1.25 * et[1] + 1e-8, (e6, et)
+
+
+@pytest.mark.gpu
+def test_x6_exact_on_integer_operands_gpu():
+    """Integer operands with exact fp32 sums: every entry point returns the exact result (the split of
+    an integer of <= 24 bits is exact, the six products carry all of it for <= 16-bit factors)."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    rows, k, n = 512, 128, 256
+    x = torch.randint(-300, 301, (rows, k), device="cuda", generator=g).float()
+    w = torch.randint(-200, 201, (n, k), device="cuda", generator=g).float()
+    exact = x.double() @ w.double().t()
+    assert float(exact.abs().max()) < 2 ** 24
+    # weight gradient: grad (rows, n) integer, x (rows, k) integer
+    gi = torch.randint(-100, 101, (rows, n), device="cuda", generator=g).float()
+    wg = weight_grad_x6(gi, x)
+    assert torch.equal(wg.double(), gi.double().t() @ x.double())
+    # backward with y = 0 (1 - y^2 = 1): gz = g W exactly; the column sums are exact too
+    gz, db = linear_tanh_backward_x6(gi, w, torch.zeros(rows, k, device="cuda"))
+    want = gi.double() @ w.double()
+    assert torch.equal(gz.double(), want)
+    assert torch.equal(db.double(), want.sum(0))
+
+
+@pytest.mark.gpu
+def test_x6_split_bound_per_product_gpu():
+    """One row (an outer product): each output is ONE product a b of full 24-bit fp32 values; the split
+    keeps it within 2^-22 |a b| (the dropped partial products are below 2^-23 |a b|, plus the fp32
+    rounding of the sum)."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    gz = torch.zeros(64, 256, device="cuda")
+    x = torch.zeros(64, 128, device="cuda")
+    gz[17] = torch.randn(256, device="cuda", generator=g) * 3.7
+    x[17] = torch.randn(128, device="cuda", generator=g) * 0.31
+    ref = gz[17].double()[:, None] * x[17].double()[None, :]
+    rel = ((weight_grad_x6(gz, x).double() - ref).abs() / ref.abs().clamp_min(1e-300)).max()
+    assert float(rel) <= 2 ** -22, float(rel)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k_out", [1, 2, 6])
+def test_x6_linear_tanh_out_gpu(k_out):
+    """The last hidden layer with the output layer folded in: y as linear_tanh_x6 (same kernel body,
+    bit for bit), the output within fp32 rounding of an fp64 evaluation on that y."""
+    g = torch.Generator(device="cuda").manual_seed(k_out)
+    rows = 2048 + 256
+    x = torch.randn(rows, 512, device="cuda", generator=g)
+    w = torch.randn(256, 512, device="cuda", generator=g) / 512 ** 0.5
+    b = torch.randn(256, device="cuda", generator=g) * 0.1
+    w_o = torch.randn(k_out, 256, device="cuda", generator=g) / 16
+    b_o = torch.randn(k_out, device="cuda", generator=g)
+    y, out = linear_tanh_out_x6(x, w, b, w_o, b_o)
+    assert torch.equal(y, linear_tanh_x6(x, w, b))
+    want = torch.addmm(b_o.double(), y.double(), w_o.double().t()).float()
+    torch.testing.assert_close(out, want, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_x6_matches_fp32_mfma_kernels_gpu():
+    """The bf16x6 and fp32-MFMA kernels compute the same functions: equal within fp32 rounding."""
+    x, w, b, gz, y_lo = _ops(4096, 512, 256, 9)
+    torch.testing.assert_close(linear_tanh_x6(x, w, b), linear_tanh(x, w, b), rtol=1e-5, atol=2e-6)
+    g6, d6 = linear_tanh_backward_x6(gz, w, y_lo)
+    gf, df = linear_tanh_backward(gz, w, y_lo)
+    torch.testing.assert_close(g6, gf, rtol=1e-5, atol=1e-5 * float(gf.abs().max()))
+    torch.testing.assert_close(d6, df, rtol=1e-5, atol=1e-5 * float(df.abs().max()))
+
+
+@pytest.mark.gpu
+def test_x6_refusals_gpu():
+    lib = N.load()
+    buf = torch.zeros(1 << 20, device="cuda")
+    p, s = buf.data_ptr(), N.stream_of(buf.device)
+    assert lib.vss_linear_tanh_bf16x6(s, 200, 512, 256, p, p, p, p) != 0      # rows % 256
+    assert lib.vss_linear_tanh_bf16x6(s, 256, 96, 256, p, p, p, p) != 0       # k % 64
+    assert lib.vss_linear_tanh_bf16x6(s, 256, 512, 200, p, p, p, p) != 0      # n % 128
+    assert lib.vss_linear_tanh_bf16x6(s, 256, 512, 256, p + 4, p, p, p) != 0  # misaligned
+    assert lib.vss_linear_tanh_out_bf16x6(s, 256, 512, 512, p, p, p, p, 2, p, p) != 0  # n_out != 256
+    assert lib.vss_linear_tanh_out_bf16x6(s, 256, 512, 256, p, p, p, p, 3, p, p) != 0  # k_out
+    assert lib.vss_linear_tanh_backward_bf16x6(s, 256, 512, 256, p, p, p, p, None) != 0
+    assert lib.vss_linear_tanh_backward_chunks_bf16x6(200, 512, 256) == -1
+    assert lib.vss_weight_grad_chunks_bf16x6(100, 256, 128) == -1
+    assert lib.vss_weight_grad_chunks_bf16x6(64, 128, 128) == -1
+    assert lib.vss_weight_grad_bf16x6(s, 64, 256, 52, p, p, p) != 0
+    assert lib.vss_weight_grad_bf16x6(s, 64, 256, 128, p, p, None) != 0

@@ -215,15 +215,17 @@ def test_fused_gemm_refusals_gpu():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("act_dim", [2, 6])
-@pytest.mark.parametrize("mlp", ["fused", "split"])
+@pytest.mark.parametrize("mlp,gemm", [("fused", "x6"), ("fused", "fp32"), ("split", "x6")])
 @pytest.mark.parametrize("rows", [256, 65536 + 64 * 3])
-def test_update_gradients_through_hip_match_autograd_gpu(rows, mlp, act_dim, monkeypatch):
+def test_update_gradients_through_hip_match_autograd_gpu(rows, mlp, gemm, act_dim, monkeypatch):
     """The update's forward equals the Agent's (bit for bit on the hipBLASLt path "split"; within
-    fp32 GEMM rounding on the fused-GEMM path); its gradients (fused HIP GEMM epilogues or the HIP
-    tanh backward + bias, split-K dW) equal autograd's up to fp32 summation order.  act_dim 6 (the
-    CMA actor: 6 output columns padded to k_pad = 8 in vss_output_backward) as well as 2 (SA/DMA:
-    k_pad = 4; the 1-column critic pads to 4 in both)."""
+    fp32 GEMM rounding on the fused-GEMM path, with the bf16x6 GEMMs where the shapes are exact --
+    all of them at 256 rows, the weight gradients only at 65,728 -- or the fp32-MFMA ones); its
+    gradients (fused HIP GEMM epilogues or the HIP tanh backward + bias, split-K dW) equal autograd's
+    up to fp32 summation order.  act_dim 6 (the CMA actor: 6 output columns padded to k_pad = 8 in
+    vss_output_backward) as well as 2 (SA/DMA: k_pad = 4; the 1-column critic pads to 4 in both)."""
     monkeypatch.setattr(P, "UPDATE_MLP", mlp)
+    monkeypatch.setattr(P, "UPDATE_GEMM", gemm)
     agent = make_agent(act_dim).cuda()
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.randn(rows, 52, device="cuda", generator=g)

@@ -326,7 +326,8 @@ int vss_output_backward(void* stream, int64_t rows, int32_t k_pad, int32_t n, co
  * vss_linear_tanh_bf16x6 / _out_bf16x6 / vss_linear_tanh_backward_bf16x6: the same contracts as
  * vss_linear_tanh / vss_linear_tanh_out / vss_linear_tanh_backward with rows % 256 == 0,
  * n_out % 128 == 0, k % 64 == 0 (k_in resp. k_next); the backward's bias gradient is the sum over the
- * vss_linear_tanh_backward_chunks_bf16x6 parts.
+ * vss_linear_tanh_backward_chunks_bf16x6 parts.  w_split: caller-owned scratch of 3 * n_out * k
+ * uint16 (16-B aligned) that the call fills with the weight's bf16 planes before its GEMM reads them.
  *
  * vss_weight_grad_bf16x6: a Linear layer's weight gradient (autograd of nn.Linear, ppo…:357)
  *   partial[s][o][i] = sum over the rows r of part s of grad[r][o] x[r][i]
@@ -336,13 +337,14 @@ int vss_output_backward(void* stream, int64_t rows, int32_t k_pad, int32_t n, co
  * grad^T x GEMM.
  * ------------------------------------------------------------------------------------------- */
 int vss_linear_tanh_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
-                           const float* bias, float* y);
+                           const float* bias, float* y, uint16_t* w_split);
 int vss_linear_tanh_out_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x,
                                const float* w, const float* bias, float* y, int32_t k_out, const float* w_out,
-                               float* out_part);
+                               float* out_part, uint16_t* w_split);
 int64_t vss_linear_tanh_backward_chunks_bf16x6(int64_t rows, int32_t k_next, int32_t n_out);
 int vss_linear_tanh_backward_bf16x6(void* stream, int64_t rows, int32_t k_next, int32_t n_out, const float* grad_next,
-                                    const float* w_next_t, const float* y, float* grad_in, float* bias_partial);
+                                    const float* w_next_t, const float* y, float* grad_in, float* bias_partial,
+                                    uint16_t* w_split);
 int64_t vss_weight_grad_chunks_bf16x6(int64_t rows, int32_t n_out, int32_t k_in);
 int vss_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_in, const float* grad, const float* x,
                            float* partial);

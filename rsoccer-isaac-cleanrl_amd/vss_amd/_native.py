@@ -153,13 +153,13 @@ def load() -> ctypes.CDLL:
     L.vss_output_backward_chunks.restype = i64
     L.vss_output_backward.argtypes = [P, i64, i32, i32, P, P, P, P, P, P]
     L.vss_output_backward.restype = ctypes.c_int
-    L.vss_linear_tanh_bf16x6.argtypes = [P, i64, i32, i32, P, P, P, P]
+    L.vss_linear_tanh_bf16x6.argtypes = [P, i64, i32, i32, P, P, P, P, P]
     L.vss_linear_tanh_bf16x6.restype = ctypes.c_int
-    L.vss_linear_tanh_out_bf16x6.argtypes = [P, i64, i32, i32, P, P, P, P, i32, P, P]
+    L.vss_linear_tanh_out_bf16x6.argtypes = [P, i64, i32, i32, P, P, P, P, i32, P, P, P]
     L.vss_linear_tanh_out_bf16x6.restype = ctypes.c_int
     L.vss_linear_tanh_backward_chunks_bf16x6.argtypes = [i64, i32, i32]
     L.vss_linear_tanh_backward_chunks_bf16x6.restype = i64
-    L.vss_linear_tanh_backward_bf16x6.argtypes = [P, i64, i32, i32, P, P, P, P, P]
+    L.vss_linear_tanh_backward_bf16x6.argtypes = [P, i64, i32, i32, P, P, P, P, P, P]
     L.vss_linear_tanh_backward_bf16x6.restype = ctypes.c_int
     L.vss_weight_grad_chunks_bf16x6.argtypes = [i64, i32, i32]
     L.vss_weight_grad_chunks_bf16x6.restype = i64

@@ -190,6 +190,11 @@ def x6_wgrad_ok(rows: int, n_out: int, k_in: int) -> bool:
         and 0 < k_in <= 4096
 
 
+def _planes(w: torch.Tensor) -> torch.Tensor:
+    """Scratch for a weight's three bf16 planes (the x6 entry points fill it before their GEMM)."""
+    return torch.empty((3, w.numel()), device=w.device, dtype=torch.int16)
+
+
 def _x6_check(name, cond, *ts):
     if not cond:
         raise ValueError(f"{name}: shape outside the bf16x6 kernels' exact shapes: {[tuple(t.shape) for t in ts]}")
@@ -207,7 +212,8 @@ def linear_tanh_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.T
     x, w, b = x.contiguous(), w.contiguous(), b.contiguous()
     y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
     N.check(N.load().vss_linear_tanh_bf16x6(N.stream_of(x.device), rows, k, n, x.data_ptr(), w.data_ptr(),
-                                            b.data_ptr(), y.data_ptr()), "vss_linear_tanh_bf16x6")
+                                            b.data_ptr(), y.data_ptr(), _planes(w).data_ptr()),
+            "vss_linear_tanh_bf16x6")
     return y
 
 
@@ -221,8 +227,8 @@ def linear_tanh_out_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out:
     y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
     part = torch.empty((n // 64, rows, k_out), device=x.device, dtype=torch.float32)
     N.check(N.load().vss_linear_tanh_out_bf16x6(N.stream_of(x.device), rows, k, n, x.data_ptr(), w.data_ptr(),
-                                                b.data_ptr(), y.data_ptr(), k_out, w_out.data_ptr(), part.data_ptr()),
-            "vss_linear_tanh_out_bf16x6")
+                                                b.data_ptr(), y.data_ptr(), k_out, w_out.data_ptr(), part.data_ptr(),
+                                                _planes(w).data_ptr()), "vss_linear_tanh_out_bf16x6")
     return y, part.sum(0).add_(b_out)
 
 
@@ -239,8 +245,8 @@ def linear_tanh_backward_x6(gz_next: torch.Tensor, w_next: torch.Tensor, y: torc
     partial = torch.empty((lib.vss_linear_tanh_backward_chunks_bf16x6(rows, k_next, n), n), device=y.device,
                           dtype=torch.float32)
     N.check(lib.vss_linear_tanh_backward_bf16x6(N.stream_of(y.device), rows, k_next, n, gz_next.data_ptr(),
-                                                w_t.data_ptr(), y.data_ptr(), gz.data_ptr(), partial.data_ptr()),
-            "vss_linear_tanh_backward_bf16x6")
+                                                w_t.data_ptr(), y.data_ptr(), gz.data_ptr(), partial.data_ptr(),
+                                                _planes(w_t).data_ptr()), "vss_linear_tanh_backward_bf16x6")
     return gz, partial.sum(0)
 
 

@@ -158,13 +158,14 @@ def test_x6_refusals_gpu():
     lib = N.load()
     buf = torch.zeros(1 << 20, device="cuda")
     p, s = buf.data_ptr(), N.stream_of(buf.device)
-    assert lib.vss_linear_tanh_bf16x6(s, 200, 512, 256, p, p, p, p) != 0      # rows % 256
-    assert lib.vss_linear_tanh_bf16x6(s, 256, 96, 256, p, p, p, p) != 0       # k % 64
-    assert lib.vss_linear_tanh_bf16x6(s, 256, 512, 200, p, p, p, p) != 0      # n % 128
-    assert lib.vss_linear_tanh_bf16x6(s, 256, 512, 256, p + 4, p, p, p) != 0  # misaligned
-    assert lib.vss_linear_tanh_out_bf16x6(s, 256, 512, 512, p, p, p, p, 2, p, p) != 0  # n_out != 256
-    assert lib.vss_linear_tanh_out_bf16x6(s, 256, 512, 256, p, p, p, p, 3, p, p) != 0  # k_out
-    assert lib.vss_linear_tanh_backward_bf16x6(s, 256, 512, 256, p, p, p, p, None) != 0
+    assert lib.vss_linear_tanh_bf16x6(s, 200, 512, 256, p, p, p, p, p) != 0      # rows % 256
+    assert lib.vss_linear_tanh_bf16x6(s, 256, 96, 256, p, p, p, p, p) != 0       # k % 64
+    assert lib.vss_linear_tanh_bf16x6(s, 256, 512, 200, p, p, p, p, p) != 0      # n % 128
+    assert lib.vss_linear_tanh_bf16x6(s, 256, 512, 256, p + 4, p, p, p, p) != 0  # misaligned
+    assert lib.vss_linear_tanh_bf16x6(s, 256, 512, 256, p, p, p, p, None) != 0  # no scratch
+    assert lib.vss_linear_tanh_out_bf16x6(s, 256, 512, 512, p, p, p, p, 2, p, p, p) != 0  # n_out != 256
+    assert lib.vss_linear_tanh_out_bf16x6(s, 256, 512, 256, p, p, p, p, 3, p, p, p) != 0  # k_out
+    assert lib.vss_linear_tanh_backward_bf16x6(s, 256, 512, 256, p, p, p, p, None, p) != 0
     assert lib.vss_linear_tanh_backward_chunks_bf16x6(200, 512, 256) == -1
     assert lib.vss_weight_grad_chunks_bf16x6(100, 256, 128) == -1
     assert lib.vss_weight_grad_chunks_bf16x6(64, 128, 128) == -1

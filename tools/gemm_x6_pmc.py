@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Profiling-only: one bf16x6 GEMM shape (GEMM_DIR=fwd|bwd|wgrad, K, N; ROWS = 2,097,152) launched REPS
+times, for rocprofv3 --pmc / --kernel-trace runs of csrc/vss_gemm_x6.hip; the summary of the passes is
+tools/gemm_x6_pmc.py --summary <dir>..."""
+import collections
+import csv
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "rsoccer-isaac-cleanrl_amd"))
+
+
+def summary(dirs):
+    m = collections.defaultdict(list)
+    for d in dirs:
+        for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
+            if "gemm_x6_kernel" in r["Kernel_Name"]:
+                m[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    m = {k: sum(v) / len(v) for k, v in m.items()}
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+        m["kernel_cycles_per_xcd"] = m["GRBM_GUI_ACTIVE"] / 8
+        m["mfma_utilization"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["kernel_cycles_per_xcd"] * 1024)
+    if "SQ_WAVE_CYCLES" in m:
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",
+                  "SQ_WAIT_INST_LDS"):
+            if c in m:
+                m[c + "_frac"] = m[c] / m["SQ_WAVE_CYCLES"]
+    print(json.dumps(m, indent=1))
+
+
+if len(sys.argv) > 2 and sys.argv[1] == "--summary":
+    summary(sys.argv[2:])
+    sys.exit(0)
+
+import torch  # noqa: E402
+
+from vss_amd.update import linear_tanh_backward_x6, linear_tanh_x6, weight_grad_x6  # noqa: E402
+
+rows = int(os.environ.get("ROWS", 2097152))
+k, n = int(os.environ.get("K", 512)), int(os.environ.get("N", 512))
+reps = int(os.environ.get("REPS", 10))
+g = torch.Generator(device="cuda").manual_seed(0)
+mode = os.environ.get("GEMM_DIR", "fwd")
+if mode == "fwd":
+    x = torch.tanh(torch.randn(rows, k, device="cuda", generator=g))
+    w = torch.randn(n, k, device="cuda", generator=g) / k ** 0.5
+    b = torch.zeros(n, device="cuda")
+    fn = lambda: linear_tanh_x6(x, w, b)  # noqa: E731
+elif mode == "bwd":
+    gn = torch.randn(rows, k, device="cuda", generator=g)
+    wn = torch.randn(k, n, device="cuda", generator=g) / k ** 0.5
+    y = torch.tanh(torch.randn(rows, n, device="cuda", generator=g))
+    fn = lambda: linear_tanh_backward_x6(gn, wn, y)  # noqa: E731
+else:
+    gz = torch.randn(rows, n, device="cuda", generator=g)
+    x = torch.tanh(torch.randn(rows, k, device="cuda", generator=g))
+    fn = lambda: weight_grad_x6(gz, x)  # noqa: E731
+for _ in range(reps):
+    fn()
+torch.cuda.synchronize()
+print("done", mode, rows, k, n, reps)

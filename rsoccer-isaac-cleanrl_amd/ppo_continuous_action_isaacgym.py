@@ -34,9 +34,9 @@ from torch.distributions.normal import Normal
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from envs._gym import Box, ObservationWrapper  # noqa: E402
-from vss_amd.update import (gemm_shape_ok, linear_tanh, linear_tanh_backward, linear_tanh_backward_x6,  # noqa: E402
-                            linear_tanh_out, linear_tanh_out_ok, linear_tanh_out_x6, linear_tanh_x6, output_backward,
-                            output_backward_ok, tanh_grad_bias, weight_grad_x6, x6_ok, x6_wgrad_ok)
+from vss_amd.update import (gemm_shape_ok, linear_tanh, linear_tanh_backward, linear_tanh_backward_mixed,  # noqa: E402
+                            linear_tanh_mixed, linear_tanh_out, linear_tanh_out_mixed, linear_tanh_out_ok,
+                            output_backward, output_backward_ok, tanh_grad_bias, weight_grad_mixed)
 
 
 def strtobool(x: str) -> bool:
@@ -196,24 +196,31 @@ class _LinearTanh(torch.autograd.Function):
 
 class _TanhMLP(torch.autograd.Function):
     """The Agent's MLP (ppo…:104-111: (Linear, Tanh) x L + Linear) as ONE autograd node for the
-    update.  Forward: each hidden layer is vss_linear_tanh (GEMM + bias + tanh in one fp32 MFMA
-    launch); the output layer is addmm, as nn.Linear issues.  Backward: every hidden tanh by
-    vss_linear_tanh_backward (the input-gradient GEMM of the layer above with the tanh derivative
-    and the bias-gradient column sums in its epilogue; the output layer's few columns zero-padded
-    to 4); weight gradients split-K as _LinearSplitK.  Inputs: x, W_0, b_0, ..., W_L, b_L."""
+    update.  Forward: each hidden layer is one GEMM launch with bias + tanh in its epilogue, the last
+    one with the output layer folded in.  Backward: the output layer and the tanh below it in one
+    streaming pass (vss_output_backward); every other hidden tanh by the input-gradient GEMM of the
+    layer above with the tanh derivative and the bias-gradient column sums in its epilogue; weight
+    gradients as split GEMMs over the rows.  UPDATE_GEMM "x6" (default) runs the GEMMs of the
+    256/512-wide layers on the bf16 matrix cores in fp32 arithmetic (csrc/vss_gemm_x6.hip; whole
+    256-row tiles, the ragged rest of a minibatch on the fp32-MFMA kernels), "fp32" on the fp32-MFMA
+    kernels (csrc/vss_update.hip) only.  Inputs: x, W_0, b_0, ..., W_L, b_L."""
 
     @staticmethod
     def forward(ctx, x, *params):
         ws, bs = params[0::2], params[1::2]
         hs = [x]
         rows = x.shape[0]
+        x6 = x.is_cuda and UPDATE_GEMM == "x6"
         for w, b in zip(ws[:-2], bs[:-2]):
-            x6 = x.is_cuda and UPDATE_GEMM == "x6" and x6_ok(rows, w.shape[1], w.shape[0])
-            hs.append((linear_tanh_x6 if x6 else linear_tanh)(hs[-1], w, b))
-        if x.is_cuda and OUTPUT_FWD and linear_tanh_out_ok(rows, ws[-2].shape[1], ws[-2].shape[0], ws[-1].shape[0]):
-            # the last hidden layer and the output layer in one launch (vss_linear_tanh_out[_bf16x6])
-            x6 = UPDATE_GEMM == "x6" and x6_ok(rows, ws[-2].shape[1], ws[-2].shape[0])
-            h, out = (linear_tanh_out_x6 if x6 else linear_tanh_out)(hs[-1], ws[-2], bs[-2], ws[-1], bs[-1])
+            hs.append((linear_tanh_mixed if x6 else linear_tanh)(hs[-1], w, b))
+        if x6 and OUTPUT_FWD:
+            # the last hidden layer and the output layer in one launch per row range (the whole 256-row
+            # tiles through vss_linear_tanh_out_bf16x6, the rest through vss_linear_tanh + addmm)
+            h, out = linear_tanh_out_mixed(hs[-1], ws[-2], bs[-2], ws[-1], bs[-1])
+            hs.append(h)
+        elif x.is_cuda and OUTPUT_FWD and linear_tanh_out_ok(rows, ws[-2].shape[1], ws[-2].shape[0], ws[-1].shape[0]):
+            # the last hidden layer and the output layer in one launch (vss_linear_tanh_out)
+            h, out = linear_tanh_out(hs[-1], ws[-2], bs[-2], ws[-1], bs[-1])
             hs.append(h)
         else:
             hs.append(linear_tanh(hs[-1], ws[-2], bs[-2]))
@@ -236,10 +243,9 @@ class _TanhMLP(torch.autograd.Function):
                 grads[2 * layer + 1] = gb
                 gz, gb, grads[2 * layer] = output_backward(gz, ws[layer], hs[layer])
                 continue
-            rows = gz.shape[0]
             x6 = gz.is_cuda and UPDATE_GEMM == "x6"
-            if x6 and x6_wgrad_ok(rows, gz.shape[1], hs[layer].shape[1]):
-                grads[2 * layer] = weight_grad_x6(gz, hs[layer])
+            if x6 and hs[layer].shape[1] % 128 == 0 and gz.shape[1] % 256 == 0:
+                grads[2 * layer] = weight_grad_mixed(gz, hs[layer])
             else:
                 grads[2 * layer] = _split_k_wgrad(gz, hs[layer])
             grads[2 * layer + 1] = gb
@@ -251,10 +257,7 @@ class _TanhMLP(torch.autograd.Function):
                 # GEMM's contraction granule, so this backward is one fused pass as well
                 pad = 4 - gz.shape[1] % 4
                 gz, w = nn.functional.pad(gz, (0, pad)), nn.functional.pad(w, (0, 0, 0, pad))
-            if x6 and x6_ok(rows, gz.shape[1], hs[layer].shape[1]):
-                gz, gb = linear_tanh_backward_x6(gz, w, hs[layer])
-            else:
-                gz, gb = linear_tanh_backward(gz, w, hs[layer])
+            gz, gb = (linear_tanh_backward_mixed if x6 else linear_tanh_backward)(gz, w, hs[layer])
         gx = gz.mm(ws[0]) if ctx.needs_input_grad[0] else None
         return (gx, *grads)
 

@@ -58,7 +58,15 @@ def _fp32_2d(name, *ts):
             raise ValueError(f"{name}: fp32 tensors only, got {t.dtype}")
 
 
-def linear_tanh(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+def _out(out, shape, like):
+    if out is None:
+        return torch.empty(shape, device=like.device, dtype=torch.float32)
+    if tuple(out.shape) != tuple(shape) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous fp32 {tuple(shape)} tensor, got {out.dtype} {tuple(out.shape)}")
+    return out
+
+
+def linear_tanh(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """tanh(x @ w.T + b) for x (rows, k), w (n, k) (nn.Linear's weight), b (n,)."""
     if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1] or b.shape != (w.shape[0],):
         raise ValueError(f"linear_tanh: x {tuple(x.shape)}, w {tuple(w.shape)}, b {tuple(b.shape)}")
@@ -70,7 +78,7 @@ def linear_tanh(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tens
     if not gemm_shape_ok(k, n):
         raise ValueError(f"vss_linear_tanh: k % 4 == 0 and n % 128 == 0 required, got k={k}, n={n}")
     lib = N.load()
-    y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
+    y = _out(out, (rows, n), x)
     if rows == 0:
         return y
     x, w, b = x.contiguous(), w.contiguous(), b.contiguous()
@@ -105,7 +113,7 @@ def linear_tanh_out(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out: to
     return y, part.sum(0).add_(b_out)
 
 
-def linear_tanh_backward(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.Tensor):
+def linear_tanh_backward(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.Tensor, out: torch.Tensor | None = None):
     """The pre-activation gradient of a tanh layer from the one of the layer above:
     gz = (gz_next @ w_next) * (1 - y^2) and db = gz.sum(0), with gz_next (rows, k_next), w_next
     (k_next, n) (the next layer's nn.Linear weight), y (rows, n) (this layer's tanh output)."""
@@ -122,7 +130,7 @@ def linear_tanh_backward(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.T
     if not gemm_shape_ok(k_next, n):
         raise ValueError(f"vss_linear_tanh_backward: k_next % 4 == 0 and n % 128 == 0 required, got {k_next}, {n}")
     lib = N.load()
-    gz = torch.empty((rows, n), device=y.device, dtype=torch.float32)
+    gz = _out(out, (rows, n), y)
     if rows == 0:
         return gz, torch.zeros(n, device=y.device, dtype=torch.float32)
     gz_next, y = gz_next.contiguous(), y.contiguous()
@@ -204,27 +212,28 @@ def _x6_check(name, cond, *ts):
             raise ValueError(f"{name}: ROCm tensors only (no CPU path)")
 
 
-def linear_tanh_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+def linear_tanh_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """linear_tanh on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_bf16x6)."""
     rows, k = x.shape
     n = w.shape[0]
     _x6_check("vss_linear_tanh_bf16x6", w.shape == (n, k) and b.shape == (n,) and x6_ok(rows, k, n), x, w, b)
     x, w, b = x.contiguous(), w.contiguous(), b.contiguous()
-    y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
+    y = _out(out, (rows, n), x)
     N.check(N.load().vss_linear_tanh_bf16x6(N.stream_of(x.device), rows, k, n, x.data_ptr(), w.data_ptr(),
                                             b.data_ptr(), y.data_ptr(), _planes(w).data_ptr()),
             "vss_linear_tanh_bf16x6")
     return y
 
 
-def linear_tanh_out_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out: torch.Tensor, b_out: torch.Tensor):
+def linear_tanh_out_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out: torch.Tensor, b_out: torch.Tensor,
+                       out: torch.Tensor | None = None):
     """linear_tanh_out on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_out_bf16x6)."""
     rows, k = x.shape
     n, k_out = w.shape[0], w_out.shape[0]
     _x6_check("vss_linear_tanh_out_bf16x6", w.shape == (n, k) and b.shape == (n,) and w_out.shape == (k_out, n)
               and b_out.shape == (k_out,) and n == 256 and k_out in (1, 2, 6) and x6_ok(rows, k, n), x, w, b, w_out)
     x, w, b, w_out = x.contiguous(), w.contiguous(), b.contiguous(), w_out.contiguous()
-    y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
+    y = _out(out, (rows, n), x)
     part = torch.empty((n // 64, rows, k_out), device=x.device, dtype=torch.float32)
     N.check(N.load().vss_linear_tanh_out_bf16x6(N.stream_of(x.device), rows, k, n, x.data_ptr(), w.data_ptr(),
                                                 b.data_ptr(), y.data_ptr(), k_out, w_out.data_ptr(), part.data_ptr(),
@@ -232,7 +241,8 @@ def linear_tanh_out_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out:
     return y, part.sum(0).add_(b_out)
 
 
-def linear_tanh_backward_x6(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.Tensor):
+def linear_tanh_backward_x6(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.Tensor,
+                            out: torch.Tensor | None = None):
     """linear_tanh_backward on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_backward_bf16x6)."""
     rows, k_next = gz_next.shape
     n = y.shape[1]
@@ -241,7 +251,7 @@ def linear_tanh_backward_x6(gz_next: torch.Tensor, w_next: torch.Tensor, y: torc
     lib = N.load()
     gz_next, y = gz_next.contiguous(), y.contiguous()
     w_t = w_next.t().contiguous()  # (n, k_next): K-contiguous
-    gz = torch.empty((rows, n), device=y.device, dtype=torch.float32)
+    gz = _out(out, (rows, n), y)
     partial = torch.empty((lib.vss_linear_tanh_backward_chunks_bf16x6(rows, k_next, n), n), device=y.device,
                           dtype=torch.float32)
     N.check(lib.vss_linear_tanh_backward_bf16x6(N.stream_of(y.device), rows, k_next, n, gz_next.data_ptr(),
@@ -263,3 +273,62 @@ def weight_grad_x6(grad: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     N.check(lib.vss_weight_grad_bf16x6(N.stream_of(x.device), rows, n_out, k_in, grad.data_ptr(), x.data_ptr(),
                                        parts.data_ptr()), "vss_weight_grad_bf16x6")
     return parts.sum(0)
+
+
+# ---- any row count: whole tiles on the bf16x6 kernels, the ragged rest on the fp32 ones --------------
+# The reference's default PPO shapes are not tile multiples (4,095 envs x 128 steps / 4 minibatches =
+# 131,040 rows): the first rows // 256 * 256 rows (// 64 * 64 for the weight gradient) go to the x6
+# kernels, the remaining < 256 (< 64) rows to the fp32-MFMA kernels / torch, into one output.
+
+def linear_tanh_mixed(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    rows, k = x.shape
+    n = w.shape[0]
+    main = rows // 256 * 256
+    if main == 0 or not x6_ok(main, k, n):
+        return linear_tanh(x, w, b)
+    y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
+    linear_tanh_x6(x[:main], w, b, out=y[:main])
+    if main < rows:
+        linear_tanh(x[main:], w, b, out=y[main:])
+    return y
+
+
+def linear_tanh_out_mixed(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out: torch.Tensor, b_out: torch.Tensor):
+    rows, k = x.shape
+    n, k_out = w.shape[0], w_out.shape[0]
+    main = rows // 256 * 256
+    if main == 0 or not x6_ok(main, k, n) or n != 256 or k_out not in (1, 2, 6):
+        y = linear_tanh(x, w, b)
+        return y, torch.addmm(b_out, y, w_out.t())
+    y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
+    _, o_main = linear_tanh_out_x6(x[:main], w, b, w_out, b_out, out=y[:main])
+    if main == rows:
+        return y, o_main
+    y_t = linear_tanh(x[main:], w, b, out=y[main:])
+    return y, torch.cat([o_main, torch.addmm(b_out, y_t, w_out.t())])
+
+
+def linear_tanh_backward_mixed(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.Tensor):
+    rows, k_next = gz_next.shape
+    n = y.shape[1]
+    main = rows // 256 * 256
+    if main == 0 or not x6_ok(main, k_next, n):
+        return linear_tanh_backward(gz_next, w_next, y)
+    gz = torch.empty((rows, n), device=y.device, dtype=torch.float32)
+    _, db = linear_tanh_backward_x6(gz_next[:main], w_next, y[:main], out=gz[:main])
+    if main < rows:
+        _, db_t = linear_tanh_backward(gz_next[main:], w_next, y[main:], out=gz[main:])
+        db = db + db_t
+    return gz, db
+
+
+def weight_grad_mixed(grad: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    rows, n_out = grad.shape
+    k_in = x.shape[1]
+    main = rows // 64 * 64
+    if main == 0 or not x6_wgrad_ok(main, n_out, k_in):
+        return grad.t().mm(x)
+    dw = weight_grad_x6(grad[:main], x[:main])
+    if main < rows:
+        dw = dw.addmm_(grad[main:].t(), x[main:])
+    return dw

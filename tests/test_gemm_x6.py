@@ -8,8 +8,9 @@ import pytest
 import torch
 
 from vss_amd import _native as N
-from vss_amd.update import (linear_tanh, linear_tanh_backward, linear_tanh_backward_x6, linear_tanh_out_x6,
-                            linear_tanh_x6, weight_grad_x6, x6_ok, x6_wgrad_ok)
+from vss_amd.update import (linear_tanh, linear_tanh_backward, linear_tanh_backward_mixed, linear_tanh_backward_x6,
+                            linear_tanh_mixed, linear_tanh_out_mixed, linear_tanh_out_x6, linear_tanh_x6,
+                            weight_grad_mixed, weight_grad_x6, x6_ok, x6_wgrad_ok)
 
 
 def test_x6_shape_predicates_cpu():
@@ -171,3 +172,33 @@ def test_x6_refusals_gpu():
     assert lib.vss_weight_grad_chunks_bf16x6(64, 128, 128) == -1
     assert lib.vss_weight_grad_bf16x6(s, 64, 256, 52, p, p, p) != 0
     assert lib.vss_weight_grad_bf16x6(s, 64, 256, 128, p, p, None) != 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [100, 256, 300, 131040])
+def test_mixed_rows_match_fp64_gpu(rows):
+    """Row counts that are not tile multiples (the reference's default minibatch: 4,095 envs x 128 / 4
+    = 131,040 rows): the whole tiles on the x6 kernels, the rest on the fp32 ones, one result --
+    within the fp32 tolerances of the single-kernel tests (and the tail rows equal to the fp32 path's
+    rows up to its own rounding)."""
+    x, w, b, gz, y_lo = _ops(rows, 512, 256, rows)
+    ref = torch.tanh(x.double() @ w.double().t() + b.double())
+    y = linear_tanh_mixed(x, w, b)
+    assert _rel(y, ref)[0] < 4e-6
+    main = rows // 256 * 256
+    torch.testing.assert_close(y[main:], linear_tanh(x[main:], w, b), rtol=0, atol=0)
+    wo = torch.randn(6, 256, device="cuda") / 16
+    bo = torch.randn(6, device="cuda") * 0.1
+    y2, o2 = linear_tanh_out_mixed(x, w, b, wo, bo)
+    assert torch.equal(y2, y)
+    torch.testing.assert_close(o2.double(), y.double() @ wo.double().t() + bo.double(), rtol=1e-5, atol=1e-5)
+    # backward from the 256-wide layer into a 512-wide tanh layer
+    w2 = torch.randn(256, 512, device="cuda") / 16
+    y512 = torch.tanh(torch.randn(rows, 512, device="cuda"))
+    g256 = torch.randn(rows, 256, device="cuda") * 1e-3
+    refb = (g256.double() @ w2.double()) * (1 - y512.double() ** 2)
+    gzm, dbm = linear_tanh_backward_mixed(g256, w2, y512)
+    assert _rel(gzm, refb)[0] < 4e-6
+    torch.testing.assert_close(dbm.double(), refb.sum(0), rtol=1e-5, atol=1e-5 * float(refb.sum(0).abs().max()))
+    refw = g256.double().t() @ x.double()
+    assert _rel(weight_grad_mixed(g256, x), refw)[0] < 4e-6

@@ -18,7 +18,7 @@ if os.environ.get("PROBE_ENV", "0") == "1":
     for _ in range(300):
         env.step(a)
     torch.cuda.synchronize()
-args = P.parse_args(["--env-id", "sa", "--num-envs", "65536", "--num-updates", os.environ.get("UPDATES", "3"),
+args = P.parse_args(["--env-id", "sa", "--num-envs", os.environ.get("NUM_ENVS", "65536"), "--num-updates", os.environ.get("UPDATES", "3"),
                      "--log", os.environ.get("PROBE_LOG", "false"), "--seed", "1", "--save-path", "/tmp/runs"])
 _, hist = P.train(args)
 for h in hist:

@@ -287,6 +287,9 @@ def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
     return {"env": "sa", "n_gpus": world, "num_envs": n_envs * world, "num_envs_per_gpu": n_envs,
             "num_steps": args.num_steps, "batch": batch, "update_epochs": args.update_epochs,
             "num_minibatches": args.num_minibatches, "dtype": "f32",
+            "update_gemm": {"x6": "fp32 arithmetic on the bf16 matrix cores (exact 3-way bf16 split, six partial "
+                                  "products, fp32 accumulation; csrc/vss_gemm_x6.hip)",
+                            "fp32": "fp32 MFMA (csrc/vss_update.hip)"}.get(P.UPDATE_GEMM, P.UPDATE_GEMM),
             "gradient_exchange": ("one flat fp32 all-reduce per minibatch "
                                   f"({dist.get_backend() if dist.is_initialized() else 'none'})") if world > 1 else "none",
             "rollout_s": roll_s, "update_s": upd_s,

@@ -57,6 +57,15 @@ else:
     gz = torch.randn(rows, n, device="cuda", generator=g)
     x = torch.tanh(torch.randn(rows, k, device="cuda", generator=g))
     fn = lambda: weight_grad_x6(gz, x)  # noqa: E731
+if os.environ.get("LIB"):  # a tools/_build variant of vss_gemm_x6.hip (new API), forward only
+    import ctypes
+    L = ctypes.CDLL(os.environ["LIB"])
+    L.vss_linear_tanh_bf16x6.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32] + [ctypes.c_void_p] * 5
+    y = torch.empty(rows, n, device="cuda")
+    ws = torch.empty(3 * n * k, device="cuda", dtype=torch.int16)
+    st = torch.cuda.current_stream().cuda_stream
+    fn = lambda: L.vss_linear_tanh_bf16x6(st, rows, k, n, x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(),  # noqa: E731
+                                          ws.data_ptr())
 for _ in range(reps):
     fn()
 torch.cuda.synchronize()

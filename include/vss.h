@@ -250,6 +250,17 @@ int vss_value_forward_masked(void* stream, int64_t rows, int32_t n_act, const fl
                              float* logprob_out, float* entropy_out, float* value_out, float* mean_out,
                              const int64_t* row_mask);
 
+/*
+ * The actor tail of Agent.get_action_and_value (ppo_continuous_action_isaacgym.py:157-164) from
+ * actor means computed elsewhere (the rollout's GEMM-chain path, vss_amd/policy.py): per row,
+ * action = mean + exp(logstd) z with z from the same Philox stream (seed, counter, row) as
+ * vss_policy_forward (or action_in when given), log-prob and entropy summed over the n_act dims.
+ * mean / action_in / action_out (rows, n_act), logprob_out / entropy_out (rows,); outputs may be NULL.
+ */
+int vss_policy_sample(void* stream, int64_t rows, int32_t n_act, const float* mean, const float* logstd, uint64_t seed,
+                      uint64_t counter, const float* action_in, float* action_out, float* logprob_out,
+                      float* entropy_out);
+
 /* ---------------------------------------------------------------------------------------------
  * PPO-update helper: the backward of a hidden layer's tanh
  * (ppo_continuous_action_isaacgym.py:104-111, autograd of nn.Tanh + nn.Linear's bias) in one pass:

@@ -280,6 +280,49 @@ __device__ __forceinline__ void normal2(uint64_t seed, uint64_t ctr, uint32_t ro
   z1 = rad * sn;
 }
 
+// get_action_and_value's tail (ppo…:157-164) for one row from its actor mean: Normal(mean,
+// exp(logstd)) sample (Philox, or the given action), log-prob and entropy summed over the action
+// dims.  torch.distributions.Normal: log_prob = -(a-mu)^2/(2 var) - log(scale) - log(sqrt(2 pi));
+// entropy = 0.5 + 0.5 log(2 pi) + log(scale).  Shared by the fused kernel and vss_policy_sample, so
+// both draw the same actions from the same (seed, counter, row).
+template <int NACT>
+__device__ __forceinline__ void actor_tail(const float (&mean)[NACT], int64_t row, const float* logstd, uint64_t seed,
+                                           uint64_t counter, const float* action_in, float* action_out,
+                                           float* logprob_out, float* entropy_out, float* mean_out) {
+  float lp = 0.0f, ent = 0.0f;
+#pragma unroll
+  for (int a = 0; a < NACT; a += 2) {
+    float z0, z1;
+    if (!action_in) normal2(seed, counter, (uint32_t)row, (uint32_t)a, z0, z1);
+#pragma unroll
+    for (int h = 0; h < 2 && a + h < NACT; ++h) {
+      const float scale = expf(logstd[a + h]);
+      const float act = action_in ? action_in[row * NACT + a + h] : mean[a + h] + scale * (h ? z1 : z0);
+      const float d = act - mean[a + h];
+      const float log_scale = logf(scale);
+      lp += -(d * d) / (2.0f * (scale * scale)) - log_scale - 0.91893853320467274f;
+      ent += 0.5f + 0.91893853320467274f + log_scale;
+      if (action_out) action_out[row * NACT + a + h] = act;
+      if (mean_out) mean_out[row * NACT + a + h] = mean[a + h];
+    }
+  }
+  if (logprob_out) logprob_out[row] = lp;
+  if (entropy_out) entropy_out[row] = ent;
+}
+
+// the same tail over rows whose actor means were computed elsewhere (the rollout's GEMM-chain path)
+template <int NACT>
+__global__ __launch_bounds__(256) void sample_kernel(int64_t rows, const float* __restrict__ mean, const float* logstd,
+                                                     uint64_t seed, uint64_t counter, const float* action_in,
+                                                     float* action_out, float* logprob_out, float* entropy_out) {
+  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (row >= rows) return;
+  float m[NACT];
+#pragma unroll
+  for (int a = 0; a < NACT; ++a) m[a] = mean[row * NACT + a];
+  actor_tail<NACT>(m, row, logstd, seed, counter, action_in, action_out, logprob_out, entropy_out, nullptr);
+}
+
 struct PolicyArgs {
   int64_t rows;
   const float* obs;
@@ -337,29 +380,9 @@ __global__ __launch_bounds__(kWaves * 64) void policy_kernel(PolicyArgs p) {
   float out[NOUT];
   mlp<NOUT>(st, 0, tails, x, out);
   if constexpr (ACTOR) {
-    if (writer) {
-      // torch.distributions.Normal: log_prob = -(a-mu)^2/(2 var) - log(scale) - log(sqrt(2 pi));
-      // entropy = 0.5 + 0.5 log(2 pi) + log(scale)
-      float lp = 0.0f, ent = 0.0f;
-#pragma unroll
-      for (int a = 0; a < NACT; a += 2) {
-        float z0, z1;
-        if (!p.action_in) normal2(p.seed, p.counter, (uint32_t)row, (uint32_t)a, z0, z1);
-#pragma unroll
-        for (int h = 0; h < 2 && a + h < NACT; ++h) {
-          const float scale = expf(p.logstd[a + h]);
-          const float act = p.action_in ? p.action_in[row * NACT + a + h] : out[a + h] + scale * (h ? z1 : z0);
-          const float d = act - out[a + h];
-          const float log_scale = logf(scale);
-          lp += -(d * d) / (2.0f * (scale * scale)) - log_scale - 0.91893853320467274f;
-          ent += 0.5f + 0.91893853320467274f + log_scale;
-          if (p.action_out) p.action_out[row * NACT + a + h] = act;
-          if (p.mean_out) p.mean_out[row * NACT + a + h] = out[a + h];
-        }
-      }
-      if (p.logprob_out) p.logprob_out[row] = lp;
-      if (p.entropy_out) p.entropy_out[row] = ent;
-    }
+    if (writer)
+      actor_tail<NACT>(out, row, p.logstd, p.seed, p.counter, p.action_in, p.action_out, p.logprob_out, p.entropy_out,
+                       p.mean_out);
   } else {
     const bool masked_out = p.row_mask && writer && p.row_mask[row] == 0;
     if (writer && !masked_out && p.value_out) p.value_out[row] = out[0];
@@ -415,6 +438,22 @@ int vss_value_forward_masked(void* stream, int64_t rows, int32_t n_act, const fl
     else hipLaunchKernelGGL((vpol::policy_kernel<6, true>), grid, block, 0, s, a);
   }
   hipLaunchKernelGGL((vpol::policy_kernel<1, false>), grid, block, 0, s, a);
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+}
+
+int vss_policy_sample(void* stream, int64_t rows, int32_t n_act, const float* mean, const float* logstd, uint64_t seed,
+                      uint64_t counter, const float* action_in, float* action_out, float* logprob_out,
+                      float* entropy_out) {
+  if (rows < 0 || !mean || !logstd || !(n_act == 2 || n_act == 6)) return VSS_E_ARG;
+  if (rows == 0) return VSS_OK;
+  const dim3 grid((unsigned)((rows + 255) / 256)), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  if (n_act == 2)
+    hipLaunchKernelGGL(vpol::sample_kernel<2>, grid, block, 0, s, rows, mean, logstd, seed, counter, action_in,
+                       action_out, logprob_out, entropy_out);
+  else
+    hipLaunchKernelGGL(vpol::sample_kernel<6>, grid, block, 0, s, rows, mean, logstd, seed, counter, action_in,
+                       action_out, logprob_out, entropy_out);
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 

@@ -424,8 +424,18 @@ class TerminalValues:
         self.term_mask[step].copy_(done)
 
     def next_values(self, fused, values, next_dones, next_obs):
-        """(T, E) next_values: the masked terminal pass where a field reset, else values[t + 1]."""
-        fused.get_value_masked(self.term_obs, self.term_mask, self.term_values.view(self.T * self.E, 1))
+        """(T, E) next_values: the masked terminal pass where a field reset, else values[t + 1].  When
+        the rollout's values come from the GEMM chain (FusedPolicy.chain_active), the reset rows are
+        gathered and evaluated by the same chain (one host sync for their count, once per rollout), so
+        next_values stays exactly critic(terminal_obs) of one evaluator."""
+        if fused.chain_active(self.E):
+            idx = self.term_mask.view(-1).nonzero().squeeze(1)
+            tv = self.term_values.view(-1)
+            if idx.numel():
+                tv.index_copy_(0, idx, fused.values_chain(self.term_obs.view(self.T * self.E, -1).index_select(0, idx))
+                               .view(-1))
+        else:
+            fused.get_value_masked(self.term_obs, self.term_mask, self.term_values.view(self.T * self.E, 1))
         v_last = fused.get_value(next_obs).view(1, self.E)
         return torch.where(next_dones.bool(), self.term_values, torch.cat([values[1:], v_last], 0))
 

@@ -33,7 +33,7 @@ CH_RX, CH_RY, CH_RQX, CH_RQY, CH_RQZ, CH_RQW, CH_RVX, CH_RVY, CH_RW = 4, 10, 16,
 EXPORTED = ("vss_abi_version", "vss_source_hash", "vss_error_string", "vss_step", "vss_step_replay", "vss_rollout", "vss_reset_dones",
             "vss_reset_dones_replay",
             "vss_compute_observations", "vss_mlp_packed_size", "vss_mlp_pack", "vss_policy_forward",
-            "vss_value_forward_masked", "vss_episode_stats", "vss_tanh_grad_chunks", "vss_tanh_grad_bias",
+            "vss_value_forward_masked", "vss_policy_sample", "vss_episode_stats", "vss_tanh_grad_chunks", "vss_tanh_grad_bias",
             "vss_linear_tanh", "vss_linear_tanh_out", "vss_linear_tanh_backward_chunks", "vss_linear_tanh_backward",
             "vss_output_backward_chunks", "vss_output_backward", "vss_linear_tanh_bf16x6",
             "vss_linear_tanh_out_bf16x6", "vss_linear_tanh_backward_chunks_bf16x6", "vss_linear_tanh_backward_bf16x6",
@@ -135,6 +135,8 @@ def load() -> ctypes.CDLL:
     L.vss_policy_forward.restype = ctypes.c_int
     L.vss_value_forward_masked.argtypes = [P, i64, i32, P, P, P, P, ctypes.c_uint64, ctypes.c_uint64] + [P] * 7
     L.vss_value_forward_masked.restype = ctypes.c_int
+    L.vss_policy_sample.argtypes = [P, i64, i32, P, P, ctypes.c_uint64, ctypes.c_uint64, P, P, P, P]
+    L.vss_policy_sample.restype = ctypes.c_int
     L.vss_episode_stats.argtypes = [P, i64] + [P] * 7
     L.vss_episode_stats.restype = ctypes.c_int
     L.vss_tanh_grad_chunks.argtypes = [i64, i32]

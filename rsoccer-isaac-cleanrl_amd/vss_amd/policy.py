@@ -9,14 +9,26 @@ as one HIP kernel on the fp32 matrix cores (csrc/vss_policy.hip, include/vss.h `
 Results equal the torch Agent's within fp32 summation-order rounding (tests/test_policy.py);
 actions are sampled from the same Normal(mean, exp(logstd)) with a Philox stream instead of
 torch's generator.  Inference only (no autograd): the PPO update keeps the torch modules.
+
+At rollout sizes (>= CHAIN_MIN_ROWS rows, e.g. 65,536 envs) the two forwards run instead as a chain
+of the update's GEMM kernels -- first layer on the fp32 MFMA kernel, the 256/512-wide layers in fp32
+arithmetic on the bf16 matrix cores (csrc/vss_gemm_x6.hip, output layer folded into the last launch)
+-- and vss_policy_sample draws the actions from the actor means with the fused kernel's Philox
+stream: 0.93 ms instead of 1.21 ms for actor + critic at 65,536 rows (profiles/r03o_*).  Smaller
+batches keep the single fused launch.  VSS_ROLLOUT_POLICY=fused forces the fused kernel.
 """
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
 from . import _native as N
+from .update import linear_tanh_mixed, linear_tanh_out_mixed
+
+CHAIN_MIN_ROWS = 16384
+ROLLOUT_POLICY = os.environ.get("VSS_ROLLOUT_POLICY", "chain")
 
 
 class FusedPolicy:
@@ -57,12 +69,39 @@ class FusedPolicy:
         self._pack(self.agent.actor_mean, self.n_act, self._actor)
         self._pack(self.agent.critic, 1, self._critic)
 
+    def _chain(self, seq, obs):
+        """One MLP's output (rows, n_out) through the update's GEMM kernels (no autograd)."""
+        lins = self._linears(seq)
+        h = obs
+        for m in lins[:-2]:
+            h = linear_tanh_mixed(h, m.weight.detach(), m.bias.detach())
+        return linear_tanh_out_mixed(h, lins[-2].weight.detach(), lins[-2].bias.detach(), lins[-1].weight.detach(),
+                                     lins[-1].bias.detach())[1]
+
+    def chain_active(self, rows: int) -> bool:
+        """Whether a batch of `rows` observations is evaluated by the GEMM chain."""
+        return ROLLOUT_POLICY == "chain" and rows >= CHAIN_MIN_ROWS
+
+    @torch.no_grad()
+    def values_chain(self, obs):
+        """critic(obs) through the GEMM chain for ANY row count, padded to whole 256-row tiles so every
+        row takes the same kernels as in a chain-sized batch: a row's value does not depend on the
+        batch it is evaluated in (the masked terminal pass of the rollout relies on it)."""
+        obs = obs.reshape(-1, 52).to(self.device, torch.float32)
+        rows = obs.shape[0]
+        pad = -rows % 256
+        if pad:
+            obs = torch.cat([obs, obs.new_zeros((pad, 52))])
+        return self._chain(self.agent.critic, obs.contiguous())[:rows]
+
     def _run(self, obs, actor: bool, action=None, out=None, want_mean=False):
         obs = obs.reshape(-1, 52)
         if obs.dtype != torch.float32 or not obs.is_contiguous() or obs.device != self.device:
             obs = obs.to(self.device, torch.float32).contiguous()
         rows = obs.shape[0]
         dev = self.device
+        if ROLLOUT_POLICY == "chain" and rows >= CHAIN_MIN_ROWS:
+            return self._run_chain(obs, actor, action, out, want_mean)
         if out is not None:
             # caller-owned outputs (the rollout storage rows): action, log-prob and value written in place
             act_out, logp, value = out
@@ -90,6 +129,35 @@ class FusedPolicy:
         if actor:
             return (action if action is not None else outs[0]), outs[1], outs[2], value, outs[3]
         return value
+
+    def _run_chain(self, obs, actor: bool, action, out, want_mean):
+        """_run through the GEMM chain + vss_policy_sample (same outputs and sampling stream)."""
+        rows, dev = obs.shape[0], self.device
+        value = self._chain(self.agent.critic, obs)
+        if not actor:
+            return value
+        mean = self._chain(self.agent.actor_mean, obs).contiguous()
+        if out is not None:
+            act_out, logp, val_out = out
+            for t, w in ((act_out, rows * self.n_act), (logp, rows), (val_out, rows)):
+                if t.numel() != w or t.dtype != torch.float32 or t.device != dev or not t.is_contiguous():
+                    raise ValueError("out buffers must be contiguous fp32 on the policy's device with one row per obs")
+            val_out.view(rows, 1).copy_(value)
+            value, ent = val_out, None
+            act_out = act_out if action is None else None
+        else:
+            act_out = torch.empty((rows, self.n_act), device=dev) if action is None else None
+            logp, ent = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+        if action is not None:
+            action = action.to(dev, torch.float32).contiguous()
+            if action.numel() != rows * self.n_act:
+                raise ValueError(f"action must have {rows} x {self.n_act} elements, got {tuple(action.shape)}")
+        self.counter += 1
+        N.check(N.load().vss_policy_sample(N.stream_of(dev), rows, self.n_act, mean.data_ptr(),
+                                           self.agent.actor_logstd.detach().data_ptr(), self.seed, self.counter,
+                                           N.ptr(action), N.ptr(act_out), logp.data_ptr(), N.ptr(ent)),
+                "vss_policy_sample")
+        return (action if action is not None else act_out), logp, ent, value, (mean if want_mean else None)
 
     @torch.no_grad()
     def get_action_and_value(self, obs, action=None, out=None):

@@ -145,3 +145,36 @@ def test_outputs_written_into_caller_buffers():
     torch.testing.assert_close(store_lp[2], lp_t, rtol=2e-5, atol=2e-5)
     with pytest.raises(ValueError):
         fused.get_action_and_value(obs, out=(store_a[2], store_lp[2][:-1], store_v[2].view(-1, 1)))
+
+
+def test_chain_path_matches_fused_kernel_and_agent():
+    """At rollout sizes the policy runs as the GEMM chain (first layer fp32 MFMA, hidden layers x6,
+    output folded) + vss_policy_sample: means / values within fp32 rounding of the fused kernel and of
+    the torch Agent, the same Philox draws (action - mean identical in distribution: with the same
+    seed and counter, the z of both paths agree to the means' rounding), entropy identical."""
+    from vss_amd import policy as PM
+    agent = make_agent(2, 21)
+    rows = PM.CHAIN_MIN_ROWS * 2
+    obs = torch.randn(rows, 52, device=DEV) * 0.7
+    chain, fused = PM.FusedPolicy(agent, seed=5), PM.FusedPolicy(agent, seed=5)
+    assert chain.chain_active(rows)
+    a_c, lp_c, ent_c, v_c = chain.get_action_and_value(obs)
+    mean_c = chain.actor_mean(obs)
+    old = PM.ROLLOUT_POLICY
+    try:
+        PM.ROLLOUT_POLICY = "fused"
+        a_f, lp_f, ent_f, v_f = fused.get_action_and_value(obs)
+        mean_f = fused.actor_mean(obs)
+    finally:
+        PM.ROLLOUT_POLICY = old
+    with torch.no_grad():
+        mean_t, v_t = agent.actor_mean(obs), agent.get_value(obs)
+    torch.testing.assert_close(mean_c, mean_t, rtol=2e-5, atol=2e-6)
+    torch.testing.assert_close(mean_c, mean_f, rtol=2e-5, atol=2e-6)
+    torch.testing.assert_close(v_c, v_t, rtol=2e-5, atol=2e-6)
+    torch.testing.assert_close(v_c, v_f, rtol=2e-5, atol=2e-6)
+    torch.testing.assert_close(a_c - mean_c, a_f - mean_f, rtol=0, atol=1e-5)  # same z
+    torch.testing.assert_close(lp_c, lp_f, rtol=2e-5, atol=2e-5)
+    assert torch.equal(ent_c, ent_f)
+    vr = chain.values_chain(obs[:1000])  # any row count: the same per-row values
+    assert torch.equal(vr, v_c[:1000])

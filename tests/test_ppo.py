@@ -210,25 +210,27 @@ def test_train_sa_65536_envs_config3(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("form", ["per_step", "batched"])
-def test_fused_rollout_next_values_equal_reference_definition(tmp_path, form):
+@pytest.mark.parametrize("form,E", [("per_step", 2048), ("batched", 2048), ("batched", 16384)])
+def test_fused_rollout_next_values_equal_reference_definition(tmp_path, form, E):
     """With the fused policy the PPO loop reconstructs next_values[t] = critic(terminal_obs_t)
     (ppo…:272) from values[t+1] and the masked terminal pass.  Check the identity directly: run a
     short SA rollout and compare with critic(terminal_obs) evaluated for every row -- with the
     masked pass once per step ("per_step") and in the form train() uses ("batched":
-    TerminalValues records every step, then ONE masked pass over all T x E rows)."""
+    TerminalValues records every step, then ONE masked pass over all T x E rows).  E = 16,384 runs
+    the policy as the GEMM chain (FusedPolicy.chain_active), whose reset rows TerminalValues gathers
+    and evaluates with the same chain."""
     from envs.vss import default_cfg
     from envs.wrappers import SingleAgent
     from envs.vss import VSS
     from vss_amd.policy import FusedPolicy
-    cfg = default_cfg(2048)
+    cfg = default_cfg(E)
     cfg["env"]["maxEpisodeLength"] = 8
     cfg["env"]["seed"] = 5
     env = VSS(cfg, "cuda:0", "cuda:0", 0, True, False, False)
     W = SingleAgent(env)
     agent = make_agent(2).cuda()
     fused = FusedPolicy(agent, seed=1)
-    T, E = 12, 2048
+    T = 12
     values = torch.zeros((T, E), device="cuda")
     term = torch.zeros((T, E), device="cuda")
     full = torch.zeros((T, E), device="cuda")

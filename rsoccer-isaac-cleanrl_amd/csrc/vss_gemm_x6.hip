@@ -343,7 +343,20 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // EPI_DTANH: the epilogue's first y row group (tj = 0) is loaded at the start of the item's last
+    // K-tile pair, so its HBM latency hides behind that pair's MFMAs instead of stalling the epilogue
+    // (a y load issued in the epilogue also waits, by vmcnt's in-order count, for the next item's
+    // prefetched K tiles)
+    f32x4 ypre[EPI == EPI_DTANH ? TI : 1];
+    const int64_t jy = (int64_t)jt * BJ + wj * C::WTJ + fr;
     for (int kt = 0; kt < a.ktiles; kt += 2) {
+      if constexpr (EPI == EPI_DTANH) {
+        if (kt + 2 >= a.ktiles) {
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+            ypre[i] = *reinterpret_cast<const f32x4*>(a.y + jy * a.ldo + it * BI + wi * C::WTI + 16 * i + 4 * fg);
+        }
+      }
       mfma_tile(0);
       swrite(r1, 1);
       __syncthreads();
@@ -384,7 +397,7 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
             }
           }
         } else if constexpr (EPI == EPI_DTANH) {
-          const f32x4 yv = *reinterpret_cast<const f32x4*>(a.y + jg * a.ldo + ig);
+          const f32x4 yv = j == 0 ? ypre[i] : *reinterpret_cast<const f32x4*>(a.y + jg * a.ldo + ig);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             v[r] = v[r] * fmaf(-yv[r], yv[r], 1.0f);

@@ -118,9 +118,10 @@ using CfgA = Cfg<128, 256, 2, 4>;
 
 struct Args {
   int32_t ni, nj;          // i tiles, j tiles (of BI, BJ)
-  int32_t ktiles;          // K tiles per work item (even)
+  int64_t kpairs;          // K-tile pairs of the whole contraction
   int32_t items;           // work items = ni * nj * splits
-  int32_t splits;          // EPI_WGRAD: contraction parts
+  int32_t splits;          // contraction parts (EPI_WGRAD; 1 otherwise): part s takes K-tile pairs
+                           // [s kpairs / splits, (s + 1) kpairs / splits)
   int64_t ldp, ldq;        // row strides (floats) of P and Q in global memory
   const void* p;           // ST_ROW: (I, K) rows; ST_TR: (K, I), i.e. rows of the contraction;
                            // ST_PRE: (3, I, K) bf16 planes (hi, mid, lo) split beforehand
@@ -264,11 +265,18 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
   int f_item = slot, f_kt = 0;
   const char* fp;
   const char* fq;
-  int64_t fk0 = 0;  // contraction offset of the item (EPI_WGRAD split)
+  // first K tile of contraction part sp (parts differ by at most one K-tile pair)
+  auto kt_lo = [&](int sp) -> int64_t {
+    if constexpr (EPI == EPI_WGRAD) return 2 * ((int64_t)sp * a.kpairs / a.splits);
+    return sp == 0 ? 0 : 2 * a.kpairs;  // one part
+  };
+  int64_t fk0 = 0;  // contraction offset of the fetched item (EPI_WGRAD part)
+  int f_kn = 0;     // its K tiles
   auto point = [&](int w) {
     int it, jt, sp;
     item_ij(w, it, jt, sp);
-    fk0 = (int64_t)sp * a.ktiles * KT;
+    fk0 = kt_lo(sp) * KT;
+    f_kn = (int)(kt_lo(sp + 1) - kt_lo(sp));
     constexpr int64_t EP = SP == ST_PRE ? 2 : 4;  // element bytes
     if constexpr (SP == ST_TR) fp = static_cast<const char*>(a.p) + (int64_t)it * BI * EP;
     else fp = static_cast<const char*>(a.p) + (int64_t)it * BI * a.ldp * EP;
@@ -280,13 +288,13 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     const int64_t k0 = fk0 + (int64_t)f_kt * KT;
     load_op<SP, BI, PI, C>(s.v, fp, a.ldp, k0, a.pps);
     load_op<SQ, BJ, PJ, C>(s.v + PI, fq, a.ldq, k0, 0);
-    if (++f_kt >= a.ktiles) {
+    if (++f_kt >= f_kn) {
       if (f_item + G < a.items) {
         f_kt = 0;
         f_item += G;
         point(f_item);
       } else {
-        f_kt = a.ktiles - 1;  // past the last item: re-load its last K tile (in bounds, never used)
+        f_kt = f_kn - 1;  // past the last item: re-load its last K tile (in bounds, never used)
       }
     }
   };
@@ -349,9 +357,10 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     // prefetched K tiles)
     f32x4 ypre[EPI == EPI_DTANH ? TI : 1];
     const int64_t jy = (int64_t)jt * BJ + wj * C::WTJ + fr;
-    for (int kt = 0; kt < a.ktiles; kt += 2) {
+    const int kn = (int)(kt_lo(sp + 1) - kt_lo(sp));  // this item's K tiles (even)
+    for (int kt = 0; kt < kn; kt += 2) {
       if constexpr (EPI == EPI_DTANH) {
-        if (kt + 2 >= a.ktiles) {
+        if (kt + 2 >= kn) {
 #pragma unroll
           for (int i = 0; i < TI; ++i)
             ypre[i] = *reinterpret_cast<const f32x4*>(a.y + jy * a.ldo + it * BI + wi * C::WTI + 16 * i + 4 * fg);
@@ -448,7 +457,8 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
 constexpr int kGridCus = 256;  // persistent grid sized for MI355X on every device (fixed partial layout)
 
 struct Plan {
-  int32_t ni, nj, ktiles, splits, items, grid;
+  int32_t ni, nj, splits, items, grid;
+  int64_t kpairs;
 };
 
 // forward / backward: exact shapes only (the update's minibatches): rows % 256, n % 128, k % 64
@@ -461,7 +471,7 @@ static Plan fb_plan(int64_t rows, int32_t k, int32_t n) {
   Plan p;
   p.ni = n / CfgA::BI;
   p.nj = (int32_t)(rows / CfgA::BJ);
-  p.ktiles = k / KT;
+  p.kpairs = k / (2 * KT);
   p.splits = 1;
   p.items = p.ni * p.nj;
   int g = kGridCus * CfgA::BPC;
@@ -471,9 +481,10 @@ static Plan fb_plan(int64_t rows, int32_t k, int32_t n) {
 }
 
 // weight gradient: dW (n_out, k_in) = grad^T x over `rows`: k_in % 128, n_out % 256, rows % 64;
-// splits S | rows / 64 so that the ni * nj * S items fill the persistent grid
+// S contraction parts so that the ni * nj * S items fill the persistent grid (S <= the K-tile pairs;
+// the parts differ by at most one pair: any row count that is a multiple of 64 fills the grid)
 static bool wg_shape_ok(int64_t rows, int32_t n_out, int32_t k_in) {
-  return rows > 0 && rows % (2 * KT) == 0 && rows <= (int64_t(1) << 40) && k_in > 0 && k_in % CfgA::BI == 0 &&
+  return rows > 0 && rows % (2 * KT) == 0 && rows <= (int64_t(1) << 36) && k_in > 0 && k_in % CfgA::BI == 0 &&
          k_in <= 4096 && n_out > 0 && n_out % CfgA::BJ == 0 && n_out <= 4096;
 }
 
@@ -483,11 +494,11 @@ static Plan wg_plan(int64_t rows, int32_t n_out, int32_t k_in) {
   p.nj = n_out / CfgA::BJ;
   const int64_t pairs = rows / (2 * KT);  // K-tile pairs
   const int tiles = p.ni * p.nj;
-  int s = kGridCus * CfgA::BPC / tiles;
+  int64_t s = kGridCus * CfgA::BPC / tiles;
   if (s < 1) s = 1;
-  while (s > 1 && pairs % s) --s;  // the largest S <= grid / tiles dividing the K-tile pairs
-  p.splits = s;
-  p.ktiles = (int32_t)(pairs / s * 2);
+  if (s > pairs) s = pairs;
+  p.splits = (int32_t)s;
+  p.kpairs = pairs;
   p.items = tiles * s;
   p.grid = p.items < kGridCus * CfgA::BPC ? p.items : kGridCus * CfgA::BPC;
   p.grid -= (p.grid % 8 && p.grid > 8) ? p.grid % 8 : 0;
@@ -498,7 +509,7 @@ template <int EPI, int SP, int SQ, int KO = 0>
 static int launch(void* stream, Args a, const Plan& pl) {
   a.ni = pl.ni;
   a.nj = pl.nj;
-  a.ktiles = pl.ktiles;
+  a.kpairs = pl.kpairs;
   a.items = pl.items;
   a.splits = pl.splits;
   hipLaunchKernelGGL((gemm_x6_kernel<EPI, SP, SQ, CfgA, KO>), dim3((unsigned)pl.grid), dim3(CfgA::THREADS), 0,

@@ -149,7 +149,7 @@ class Agent(nn.Module):
 # ~150 TF (tools/wgrad_bench.py): -0.9 s per update.  Forward and input gradient are unchanged
 # (addmm with bias = what nn.Linear issues; dY W); only the fp32 summation order of dW differs.
 SPLITK = 64
-SPLITK_MIN_ROWS = 65536
+SPLITK_MIN_ROWS = 32768
 TANH_GRAD_COLS = (64, 128, 256, 512, 1024)  # widths vss_tanh_grad_bias takes (the Agent's: 256, 512)
 
 
@@ -168,9 +168,12 @@ class _LinearSplitK(torch.autograd.Function):
 
 def _split_k_wgrad(gz, x):
     rows = x.shape[0]
-    if rows >= SPLITK_MIN_ROWS and rows % SPLITK == 0:
-        return torch.bmm(gz.reshape(SPLITK, rows // SPLITK, gz.shape[1]).transpose(1, 2),
-                         x.reshape(SPLITK, rows // SPLITK, x.shape[1])).sum(0)
+    if rows >= SPLITK_MIN_ROWS:
+        # the rows in SPLITK equal chunks (one batched GEMM + a sum), the < SPLITK left over added
+        main = rows // SPLITK * SPLITK
+        dw = torch.bmm(gz[:main].reshape(SPLITK, main // SPLITK, gz.shape[1]).transpose(1, 2),
+                       x[:main].reshape(SPLITK, main // SPLITK, x.shape[1])).sum(0)
+        return dw.addmm_(gz[main:].t(), x[main:]) if main < rows else dw
     return gz.t().mm(x)
 
 

@@ -278,7 +278,9 @@ def weight_grad_x6(grad: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
 # ---- any row count: whole tiles on the bf16x6 kernels, the ragged rest on the fp32 ones --------------
 # The reference's default PPO shapes are not tile multiples (4,095 envs x 128 steps / 4 minibatches =
 # 131,040 rows): the first rows // 256 * 256 rows (// 64 * 64 for the weight gradient) go to the x6
-# kernels, the remaining < 256 (< 64) rows to the fp32-MFMA kernels / torch, into one output.
+# kernels, the remaining < 256 (< 64) rows to hipBLASLt (torch addmm / mm, plain fp32 GEMMs) into the
+# same output -- a persistent kernel on one or two row tiles would run latency-bound (the masked
+# fp32-MFMA kernels took 120-128 us on a 224-row tail, profiles/r03r_*).
 
 def linear_tanh_mixed(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     rows, k = x.shape
@@ -289,7 +291,7 @@ def linear_tanh_mixed(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torc
     y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
     linear_tanh_x6(x[:main], w, b, out=y[:main])
     if main < rows:
-        linear_tanh(x[main:], w, b, out=y[main:])
+        torch.addmm(b, x[main:], w.t(), out=y[main:]).tanh_()
     return y
 
 
@@ -304,7 +306,7 @@ def linear_tanh_out_mixed(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_o
     _, o_main = linear_tanh_out_x6(x[:main], w, b, w_out, b_out, out=y[:main])
     if main == rows:
         return y, o_main
-    y_t = linear_tanh(x[main:], w, b, out=y[main:])
+    y_t = torch.addmm(b, x[main:], w.t(), out=y[main:]).tanh_()
     return y, torch.cat([o_main, torch.addmm(b_out, y_t, w_out.t())])
 
 
@@ -317,8 +319,9 @@ def linear_tanh_backward_mixed(gz_next: torch.Tensor, w_next: torch.Tensor, y: t
     gz = torch.empty((rows, n), device=y.device, dtype=torch.float32)
     _, db = linear_tanh_backward_x6(gz_next[:main], w_next, y[:main], out=gz[:main])
     if main < rows:
-        _, db_t = linear_tanh_backward(gz_next[main:], w_next, y[main:], out=gz[main:])
-        db = db + db_t
+        y_t = y[main:]
+        gz_t = torch.mm(gz_next[main:], w_next, out=gz[main:]).mul_(1.0 - y_t * y_t)
+        db = db + gz_t.sum(0)
     return gz, db
 
 

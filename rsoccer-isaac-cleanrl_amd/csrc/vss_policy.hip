@@ -43,6 +43,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kIn = 52, kH1 = 256, kH2 = 512, kH3 = 512, kH4 = 256;
 constexpr int kWaves = 4;          // waves per workgroup (64 rows per workgroup), one per SIMD
+constexpr int64_t kBothMaxWorkgroups = 128;  // up to 8,192 rows: actor and critic in one launch
 constexpr int kRowsPerWave = 16;
 constexpr int kTiles = 16;                         // output tiles of one pass (256 features)
 constexpr int kStepFloats = kTiles * 16 * 4;       // one pass's weights for one k-step: 1,024 floats
@@ -346,17 +347,16 @@ struct PolicyArgs {
 // only the masked rows).  One network per launch keeps the weight stream that the concurrently running
 // workgroups read at 2.1 MB, inside one XCD's 4 MB L2 (actor + critic in one launch stream 4.3 MB and
 // measured 2.6 % slower: profiles/r03f_policy_bench.log).
+// One network (ACTOR: the actor and the sampling tail; else the critic) on workgroup `blk`'s rows.
 template <int NACT, bool ACTOR>
-__global__ __launch_bounds__(kWaves * 64) void policy_kernel(PolicyArgs p) {
+__device__ __forceinline__ void policy_body(const PolicyArgs& p, int64_t blk, f32x4* lds, float* tails) {
   constexpr int NOUT = ACTOR ? NACT : 1;
-  __shared__ __attribute__((aligned(16))) f32x4 lds[2 * kChunkF4];
-  __shared__ __attribute__((aligned(16))) float tails[tail_floats(NOUT)];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t r0 = ((int64_t)blockIdx.x * kWaves + wave) * kRowsPerWave;
+  const int64_t r0 = (blk * kWaves + wave) * kRowsPerWave;
   // waves past the last row still take part in the weight staging and barriers
   if (!ACTOR && p.row_mask) {
     // masked terminal-value pass: a workgroup with no masked row has nothing to do (uniform exit)
-    const int64_t wr = (int64_t)blockIdx.x * kWaves * kRowsPerWave + threadIdx.x;
+    const int64_t wr = blk * kWaves * kRowsPerWave + threadIdx.x;
     const bool m = threadIdx.x < kWaves * kRowsPerWave && wr < p.rows && p.row_mask[wr] != 0;
     if (__syncthreads_or(m) == 0) return;
   }
@@ -387,6 +387,27 @@ __global__ __launch_bounds__(kWaves * 64) void policy_kernel(PolicyArgs p) {
     const bool masked_out = p.row_mask && writer && p.row_mask[row] == 0;
     if (writer && !masked_out && p.value_out) p.value_out[row] = out[0];
   }
+}
+
+template <int NACT, bool ACTOR>
+__global__ __launch_bounds__(kWaves * 64) void policy_kernel(PolicyArgs p) {
+  __shared__ __attribute__((aligned(16))) f32x4 lds[2 * kChunkF4];
+  __shared__ __attribute__((aligned(16))) float tails[tail_floats(ACTOR ? NACT : 1)];
+  policy_body<NACT, ACTOR>(p, blockIdx.x, lds, tails);
+}
+
+// Actor and critic in ONE launch (the first half of the grid runs the actor, the second the critic):
+// for small batches (the reference's 4,095 envs: 64 workgroups per network) the two networks then
+// run side by side on 128 CUs instead of one after the other, each launch latency-bound on its
+// 66-chunk weight stream.  At 65,536 rows two launches measured 2.6 % faster (the concurrently
+// read weight stream stays in one XCD's L2), and the rollout uses the GEMM chain there anyway.
+template <int NACT>
+__global__ __launch_bounds__(kWaves * 64) void policy_kernel_both(PolicyArgs p) {
+  __shared__ __attribute__((aligned(16))) f32x4 lds[2 * kChunkF4];
+  __shared__ __attribute__((aligned(16))) float tails[tail_floats(NACT)];
+  const int64_t half = gridDim.x / 2;
+  if ((int64_t)blockIdx.x < half) policy_body<NACT, true>(p, blockIdx.x, lds, tails);
+  else policy_body<NACT, false>(p, (int64_t)blockIdx.x - half, lds, tails);
 }
 
 }  // namespace vpol
@@ -431,8 +452,15 @@ int vss_value_forward_masked(void* stream, int64_t rows, int32_t n_act, const fl
   vpol::PolicyArgs a{rows, obs, actor_packed, critic_packed, logstd, action_in, action_out, logprob_out,
                      entropy_out, value_out, mean_out, seed, counter, row_mask};
   const int64_t waves = (rows + vpol::kRowsPerWave - 1) / vpol::kRowsPerWave;
-  const dim3 grid((unsigned)((waves + vpol::kWaves - 1) / vpol::kWaves)), block(vpol::kWaves * 64);
+  const int64_t wgs = (waves + vpol::kWaves - 1) / vpol::kWaves;
+  const dim3 grid((unsigned)wgs), block(vpol::kWaves * 64);
   hipStream_t s = (hipStream_t)stream;
+  if (!critic_only && wgs <= vpol::kBothMaxWorkgroups) {  // small batch: both networks in one launch
+    const dim3 grid2((unsigned)(2 * wgs));
+    if (n_act == 2) hipLaunchKernelGGL((vpol::policy_kernel_both<2>), grid2, block, 0, s, a);
+    else hipLaunchKernelGGL((vpol::policy_kernel_both<6>), grid2, block, 0, s, a);
+    return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+  }
   if (!critic_only) {
     if (n_act == 2) hipLaunchKernelGGL((vpol::policy_kernel<2, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((vpol::policy_kernel<6, true>), grid, block, 0, s, a);

@@ -11,7 +11,7 @@ import torch  # noqa: E402
 
 import ppo_continuous_action_isaacgym as P  # noqa: E402
 from vss_amd.policy import FusedPolicy  # noqa: E402
-from vss_amd.update import linear_tanh, linear_tanh_out_x6, linear_tanh_x6  # noqa: E402
+from vss_amd.update import linear_tanh, linear_tanh_mixed as linear_tanh_x6, linear_tanh_out_mixed as linear_tanh_out_x6  # noqa: E402
 
 from collections import namedtuple  # noqa: E402
 

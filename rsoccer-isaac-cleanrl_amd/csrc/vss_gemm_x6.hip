@@ -51,7 +51,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 enum { EPI_TANH = 0, EPI_DTANH = 1, EPI_TANH_OUT = 2, EPI_WGRAD = 3 };
-enum { ST_ROW = 0, ST_TR = 1, ST_PRE = 2 };
+enum { ST_ROW = 0, ST_TR = 1, ST_PRE = 2, ST_DMA = 3 };
 
 constexpr int KT = 32;  // K tile = one v_mfma_f32_16x16x32_bf16 step
 
@@ -136,11 +136,11 @@ struct Args {
   float* out_part;         // EPI_TANH_OUT: (I / 64, J, KO)
 };
 
-// one thread's operands of one K tile: PI + PJ groups of 8, as raw fp32 bits (slots 0, 1: ST_ROW /
-// ST_TR) or as the three bf16 planes (slots 0, 1, 2: ST_PRE)
-template <class C>
+// one thread's register-staged operands of one K tile: NP groups of 8, as raw fp32 bits (slots 0, 1:
+// ST_ROW / ST_TR) or as the three bf16 planes (slots 0, 1, 2: ST_PRE)
+template <int NP>
 struct Stage {
-  u32x4 v[C::PI + C::PJ][3];
+  u32x4 v[NP][3];
 };
 
 template <int MODE, int R, int NP, class C>
@@ -200,6 +200,33 @@ __device__ __forceinline__ void write_op(const u32x4 (*src)[3], char* img) {
   }
 }
 
+// W (n, K) fp32 -> the LDS images of its three bf16 planes, tile by tile (ST_DMA): for i tile it
+// (128 rows) and K tile kt, [plane][k group g][row r][8 bf16] of W[128 it + r][32 kt + 8 g + e] --
+// exactly the bytes of the GEMM's P image, so each wave copies its slice with global_load_lds_dwordx4
+// (1 KB per wave instruction, contiguous in global memory and LDS)
+__global__ __launch_bounds__(256) void split_image_kernel(const float* __restrict__ w, int64_t n, int64_t k,
+                                                          uint16_t* __restrict__ img) {
+  const int64_t ktn = k / KT, units = n * k / 8;
+  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (it, kt, g, r), r fastest
+  if (u >= units) return;
+  const int r = (int)(u % 128), g = (int)((u / 128) % 4);
+  const int64_t kt = (u / 512) % ktn, it = u / (512 * ktn);
+  const float* src = w + (it * 128 + r) * k + kt * KT + 8 * g;
+  const u32x4 a = *reinterpret_cast<const u32x4*>(src), b = *reinterpret_cast<const u32x4*>(src + 4);
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = __uint_as_float(a[e]);
+    v[4 + e] = __uint_as_float(b[e]);
+  }
+  u32x4 hi, mid, lo;
+  split8(v, hi, mid, lo);
+  uint16_t* d = img + (it * ktn + kt) * (3 * 4 * 128 * 8) + (g * 128 + r) * 8;
+  *reinterpret_cast<u32x4*>(d) = hi;
+  *reinterpret_cast<u32x4*>(d + 4 * 128 * 8) = mid;
+  *reinterpret_cast<u32x4*>(d + 2 * 4 * 128 * 8) = lo;
+}
+
 // W (rows, K) fp32 -> its three bf16 planes (3, rows, K) (split8 on groups of 8 consecutive floats):
 // the GEMMs' weight operand is split once per call instead of once per block and tile
 __global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ src, int64_t groups,
@@ -235,9 +262,17 @@ __device__ __forceinline__ float row16_sum(float v) {
 
 template <int EPI, int SP, int SQ, class C, int KO = 0>
 __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
-  constexpr int BI = C::BI, BJ = C::BJ, TI = C::TI, TJ = C::TJ, PI = C::PI, PJ = C::PJ;
-  __shared__ __attribute__((aligned(16))) char lds[C::LDS];
-  __shared__ float epi_lds[EPI == EPI_TANH_OUT ? KO * 256 + BI : (EPI == EPI_WGRAD ? 1 : BI)];
+  constexpr int BI = C::BI, BJ = C::BJ, TI = C::TI, TJ = C::TJ, PJ = C::PJ;
+  // ST_DMA: the weight operand's image is copied global -> LDS by the waves' global_load_lds (3 KB per
+  // wave per K tile), only the activations go through registers
+  constexpr bool PDMA = SP == ST_DMA;
+  constexpr int PI = PDMA ? 0 : C::PI;
+  static_assert(!PDMA || (BI == 128 && Img<BI>::BYTES == (C::THREADS / 64) * 3 * 1024), "DMA slices: 3 KB per wave");
+  constexpr int EPI_FLOATS = EPI == EPI_TANH_OUT ? KO * 256 + BI : (EPI == EPI_WGRAD ? 1 : BI);
+  // one LDS object (a second __shared__ array beside a global_load_lds target can make hipcc wait
+  // vmcnt(0) before the k-steps' LDS reads, cdna_hip_programming.md §5)
+  __shared__ __attribute__((aligned(16))) char lds[C::LDS + EPI_FLOATS * 4];
+  float* epi_lds = reinterpret_cast<float*>(lds + C::LDS);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wi = wv / C::WJ, wj = wv % C::WJ;
   const int G = gridDim.x;
   const int slot = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
@@ -284,9 +319,9 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     else fq = reinterpret_cast<const char*>(a.q) + (int64_t)jt * BJ * a.ldq * 4;
   };
   point(f_item);
-  auto gload = [&](Stage<C>& s) {
+  auto gload = [&](Stage<PI + PJ>& s) {
     const int64_t k0 = fk0 + (int64_t)f_kt * KT;
-    load_op<SP, BI, PI, C>(s.v, fp, a.ldp, k0, a.pps);
+    if constexpr (!PDMA) load_op<SP, BI, PI, C>(s.v, fp, a.ldp, k0, a.pps);
     load_op<SQ, BJ, PJ, C>(s.v + PI, fq, a.ldq, k0, 0);
     if (++f_kt >= f_kn) {
       if (f_item + G < a.items) {
@@ -298,15 +333,32 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
       }
     }
   };
-  auto swrite = [&](const Stage<C>& s, int buf) {
+  auto swrite = [&](const Stage<PI + PJ>& s, int buf) {
     char* base = lds + buf * C::BUF;
-    write_op<SP, BI, PI, C>(s.v, base);
+    if constexpr (!PDMA) write_op<SP, BI, PI, C>(s.v, base);
     write_op<SQ, BJ, PJ, C>(s.v + PI, base + Img<BI>::BYTES);
+  };
+  // ST_DMA: K tile kt of the block's i tile it0 -> the P image of LDS buffer buf
+  auto dma_p = [&](int64_t kt, int buf) {
+    if constexpr (PDMA) {
+      const int64_t off = ((int64_t)it0 * (2 * a.kpairs) + kt) * Img<BI>::BYTES;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int slice = (wv * 3 + q) * 1024;
+        // (C-style casts: the builtin takes a global and an LDS address-space pointer)
+        __builtin_amdgcn_global_load_lds(
+            (__attribute__((address_space(1))) void*)(static_cast<const char*>(a.p) + off + slice + lane * 16),
+            (__attribute__((address_space(3))) void*)(lds + buf * C::BUF + slice), 16, 0, 0);
+      }
+    }
   };
 
   f32x4 acc[TI][TJ];
   const int fr = lane & 15, fg = lane >> 4;  // fragment row, k group
-  auto mfma_tile = [&](int buf) {
+  // the K tile in LDS buffer buf; `between` runs after its fragment reads are issued and before its
+  // MFMAs (ST_DMA: the next P image's global_load_lds, kept behind the reads so that hipcc's
+  // LDS-alias wait for the DMA does not land before them)
+  auto mfma_tile = [&](int buf, auto&& between) {
     const char* pb = lds + buf * C::BUF + fg * Img<BI>::GS + (wi * C::WTI + fr) * 16;
     const char* qb = lds + buf * C::BUF + Img<BI>::BYTES + fg * Img<BJ>::GS + (wj * C::WTJ + fr) * 16;
     u32x4 pf[3][TI], qf[3][TJ];
@@ -316,6 +368,11 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
       for (int i = 0; i < TI; ++i) pf[pl][i] = *reinterpret_cast<const u32x4*>(pb + pl * Img<BI>::PS + i * 256);
 #pragma unroll
       for (int j = 0; j < TJ; ++j) qf[pl][j] = *reinterpret_cast<const u32x4*>(qb + pl * Img<BJ>::PS + j * 256);
+    }
+    if constexpr (PDMA) {
+      __builtin_amdgcn_sched_barrier(0);
+      between();
+      __builtin_amdgcn_sched_barrier(0);
     }
     // the six products, smallest first: lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi
     constexpr int PP[6] = {2, 0, 1, 1, 0, 0};
@@ -335,8 +392,9 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
 #pragma unroll
   for (int i = 0; i < (EPI == EPI_DTANH ? TI : 1); ++i) csum[i][0] = csum[i][1] = csum[i][2] = csum[i][3] = 0.f;
 
-  Stage<C> r0, r1;
+  Stage<PI + PJ> r0, r1;
   gload(r0);  // K tile 0
+  dma_p(0, 0);
   swrite(r0, 0);
   gload(r1);  // K tile 1
   gload(r0);  // K tile 2
@@ -366,11 +424,14 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
             ypre[i] = *reinterpret_cast<const f32x4*>(a.y + jy * a.ldo + it * BI + wi * C::WTI + 16 * i + 4 * fg);
         }
       }
-      mfma_tile(0);
+      mfma_tile(0, [&] { dma_p(kt + 1, 1); });
       swrite(r1, 1);
       __syncthreads();
       gload(r1);
-      mfma_tile(1);
+      mfma_tile(1, [&] {
+        if (kt + 2 < kn) dma_p(kt + 2, 0);
+        else if (has_next) dma_p(0, 0);  // the next item's first K tile (same i tile, all K tiles)
+      });
       swrite(r0, 0);
       __syncthreads();
       gload(r0);
@@ -519,11 +580,12 @@ static int launch(void* stream, Args a, const Plan& pl) {
 
 static bool misaligned(const void* p) { return !p || (reinterpret_cast<uintptr_t>(p) & 15) != 0; }
 
-// the weight operand's planes: w (n, k) fp32 -> w_split (3, n, k) bf16, then the GEMM reads them
+// the weight operand's planes: w (n, k) fp32 -> w_split, the tile-ordered LDS images of its bf16
+// planes (3 n k uint16, split_image_kernel), which the GEMM copies with global_load_lds
 static int split_weight(void* stream, const float* w, int64_t n, int64_t k, uint16_t* w_split) {
-  const int64_t groups = n * k / 8;
-  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, (hipStream_t)stream, w,
-                     groups, w_split);
+  const int64_t units = n * k / 8;
+  hipLaunchKernelGGL(split_image_kernel, dim3((unsigned)((units + 255) / 256)), dim3(256), 0, (hipStream_t)stream, w, n,
+                     k, w_split);
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 
@@ -553,7 +615,7 @@ int vss_linear_tanh_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_o
   if (rc != VSS_OK) return rc;
   Args a = fb_args(k_in, n_out, w_split, x, y);
   a.bias = bias;
-  return launch<EPI_TANH, ST_PRE, ST_ROW>(stream, a, fb_plan(rows, k_in, n_out));
+  return launch<EPI_TANH, ST_DMA, ST_ROW>(stream, a, fb_plan(rows, k_in, n_out));
 }
 
 int vss_linear_tanh_out_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
@@ -570,9 +632,9 @@ int vss_linear_tanh_out_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t
   a.w_out = w_out;
   a.out_part = out_part;
   const Plan pl = fb_plan(rows, k_in, n_out);
-  if (k_out == 1) return launch<EPI_TANH_OUT, ST_PRE, ST_ROW, 1>(stream, a, pl);
-  if (k_out == 2) return launch<EPI_TANH_OUT, ST_PRE, ST_ROW, 2>(stream, a, pl);
-  return launch<EPI_TANH_OUT, ST_PRE, ST_ROW, 6>(stream, a, pl);
+  if (k_out == 1) return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, 1>(stream, a, pl);
+  if (k_out == 2) return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, 2>(stream, a, pl);
+  return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, 6>(stream, a, pl);
 }
 
 int64_t vss_linear_tanh_backward_chunks_bf16x6(int64_t rows, int32_t k_next, int32_t n_out) {
@@ -594,7 +656,7 @@ int vss_linear_tanh_backward_bf16x6(void* stream, int64_t rows, int32_t k_next, 
   Args a = fb_args(k_next, n_out, w_split, grad_next, grad_in);
   a.y = y;
   a.partial = bias_partial;
-  return launch<EPI_DTANH, ST_PRE, ST_ROW>(stream, a, fb_plan(rows, k_next, n_out));
+  return launch<EPI_DTANH, ST_DMA, ST_ROW>(stream, a, fb_plan(rows, k_next, n_out));
 }
 
 int64_t vss_weight_grad_chunks_bf16x6(int64_t rows, int32_t n_out, int32_t k_in) {

@@ -51,7 +51,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 enum { EPI_TANH = 0, EPI_DTANH = 1, EPI_TANH_OUT = 2, EPI_WGRAD = 3 };
-enum { ST_ROW = 0, ST_TR = 1, ST_PRE = 2, ST_DMA = 3 };
+enum { ST_ROW = 0, ST_TR = 1, ST_DMA = 2 };
 
 constexpr int KT = 32;  // K tile = one v_mfma_f32_16x16x32_bf16 step
 
@@ -123,9 +123,8 @@ struct Args {
   int32_t splits;          // contraction parts (EPI_WGRAD; 1 otherwise): part s takes K-tile pairs
                            // [s kpairs / splits, (s + 1) kpairs / splits)
   int64_t ldp, ldq;        // row strides (floats) of P and Q in global memory
-  const void* p;           // ST_ROW: (I, K) rows; ST_TR: (K, I), i.e. rows of the contraction;
-                           // ST_PRE: (3, I, K) bf16 planes (hi, mid, lo) split beforehand
-  int64_t pps;             // ST_PRE: plane stride (elements)
+  const void* p;           // ST_TR: (K, I), i.e. rows of the contraction; ST_DMA: the tile-ordered
+                           // LDS images of the (I, K) weight's bf16 planes (split_image_kernel)
   const float* q;          // ST_ROW: (J, K);      ST_TR: (K, J)
   int64_t ldo;             // output row stride (floats): out[j][i]
   float* out;              // (J, I) (EPI_WGRAD: (splits, J, I))
@@ -136,15 +135,14 @@ struct Args {
   float* out_part;         // EPI_TANH_OUT: (I / 64, J, KO)
 };
 
-// one thread's register-staged operands of one K tile: NP groups of 8, as raw fp32 bits (slots 0, 1:
-// ST_ROW / ST_TR) or as the three bf16 planes (slots 0, 1, 2: ST_PRE)
+// one thread's register-staged operands of one K tile: NP groups of 8 raw fp32 values
 template <int NP>
 struct Stage {
-  u32x4 v[NP][3];
+  u32x4 v[NP][2];
 };
 
 template <int MODE, int R, int NP, class C>
-__device__ __forceinline__ void load_op(u32x4 (*dst)[3], const void* base_, int64_t ld, int64_t k0, int64_t pps) {
+__device__ __forceinline__ void load_op(u32x4 (*dst)[2], const void* base_, int64_t ld, int64_t k0) {
   const int t = threadIdx.x;
 #pragma unroll
   for (int u = 0; u < NP; ++u) {
@@ -154,11 +152,6 @@ __device__ __forceinline__ void load_op(u32x4 (*dst)[3], const void* base_, int6
       const float* src = static_cast<const float*>(base_) + (int64_t)row * ld + k0 + 8 * g;
       dst[u][0] = *reinterpret_cast<const u32x4*>(src);
       dst[u][1] = *reinterpret_cast<const u32x4*>(src + 4);
-    } else if constexpr (MODE == ST_PRE) {
-      const int g = (pr >> 3) & 3, row = (pr & 7) | ((pr >> 5) << 3);
-      const uint16_t* src = static_cast<const uint16_t*>(base_) + (int64_t)row * ld + k0 + 8 * g;
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) dst[u][pl] = *reinterpret_cast<const u32x4*>(src + pl * pps);
     } else {
       const int row = pr % R, g = pr / R;
       const float* src = static_cast<const float*>(base_) + (k0 + 8 * g) * ld + row;
@@ -169,7 +162,7 @@ __device__ __forceinline__ void load_op(u32x4 (*dst)[3], const void* base_, int6
 }
 
 template <int MODE, int R, int NP, class C>
-__device__ __forceinline__ void write_op(const u32x4 (*src)[3], char* img) {
+__device__ __forceinline__ void write_op(const u32x4 (*src)[2], char* img) {
   const int t = threadIdx.x;
 #pragma unroll
   for (int u = 0; u < NP; ++u) {
@@ -183,16 +176,10 @@ __device__ __forceinline__ void write_op(const u32x4 (*src)[3], char* img) {
       row = (pr & 7) | ((pr >> 5) << 3);
     }
     u32x4 hi, mid, lo;
-    if constexpr (MODE == ST_PRE) {
-      hi = src[u][0];
-      mid = src[u][1];
-      lo = src[u][2];
-    } else {
-      float v[8];
+    float v[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(src[u][e >> 2][e & 3]);
-      split8(v, hi, mid, lo);
-    }
+    for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(src[u][e >> 2][e & 3]);
+    split8(v, hi, mid, lo);
     char* d = img + g * Img<R>::GS + row * 16;
     *reinterpret_cast<u32x4*>(d) = hi;
     *reinterpret_cast<u32x4*>(d + Img<R>::PS) = mid;
@@ -225,26 +212,6 @@ __global__ __launch_bounds__(256) void split_image_kernel(const float* __restric
   *reinterpret_cast<u32x4*>(d) = hi;
   *reinterpret_cast<u32x4*>(d + 4 * 128 * 8) = mid;
   *reinterpret_cast<u32x4*>(d + 2 * 4 * 128 * 8) = lo;
-}
-
-// W (rows, K) fp32 -> its three bf16 planes (3, rows, K) (split8 on groups of 8 consecutive floats):
-// the GEMMs' weight operand is split once per call instead of once per block and tile
-__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ src, int64_t groups,
-                                                           uint16_t* __restrict__ dst) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= groups) return;
-  const u32x4 a = *reinterpret_cast<const u32x4*>(src + 8 * i), b = *reinterpret_cast<const u32x4*>(src + 8 * i + 4);
-  float v[8];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    v[e] = __uint_as_float(a[e]);
-    v[4 + e] = __uint_as_float(b[e]);
-  }
-  u32x4 hi, mid, lo;
-  split8(v, hi, mid, lo);
-  *reinterpret_cast<u32x4*>(dst + 8 * i) = hi;
-  *reinterpret_cast<u32x4*>(dst + 8 * (groups + i)) = mid;
-  *reinterpret_cast<u32x4*>(dst + 8 * (2 * groups + i)) = lo;
 }
 
 // sum over the 16 lanes of a DPP row (as vss_update.hip row16_sum)
@@ -312,17 +279,16 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     item_ij(w, it, jt, sp);
     fk0 = kt_lo(sp) * KT;
     f_kn = (int)(kt_lo(sp + 1) - kt_lo(sp));
-    constexpr int64_t EP = SP == ST_PRE ? 2 : 4;  // element bytes
-    if constexpr (SP == ST_TR) fp = static_cast<const char*>(a.p) + (int64_t)it * BI * EP;
-    else fp = static_cast<const char*>(a.p) + (int64_t)it * BI * a.ldp * EP;
+    if constexpr (SP == ST_TR) fp = static_cast<const char*>(a.p) + (int64_t)it * BI * 4;
+    else fp = static_cast<const char*>(a.p);  // ST_DMA: addressed by dma_p
     if constexpr (SQ == ST_TR) fq = reinterpret_cast<const char*>(a.q) + (int64_t)jt * BJ * 4;
     else fq = reinterpret_cast<const char*>(a.q) + (int64_t)jt * BJ * a.ldq * 4;
   };
   point(f_item);
   auto gload = [&](Stage<PI + PJ>& s) {
     const int64_t k0 = fk0 + (int64_t)f_kt * KT;
-    if constexpr (!PDMA) load_op<SP, BI, PI, C>(s.v, fp, a.ldp, k0, a.pps);
-    load_op<SQ, BJ, PJ, C>(s.v + PI, fq, a.ldq, k0, 0);
+    if constexpr (!PDMA) load_op<SP, BI, PI, C>(s.v, fp, a.ldp, k0);
+    load_op<SQ, BJ, PJ, C>(s.v + PI, fq, a.ldq, k0);
     if (++f_kt >= f_kn) {
       if (f_item + G < a.items) {
         f_kt = 0;
@@ -595,7 +561,6 @@ static Args fb_args(int32_t k, int32_t n, const uint16_t* w_split, const float* 
   a.ldp = k;
   a.ldq = k;
   a.p = w_split;
-  a.pps = (int64_t)n * k;
   a.q = q;
   a.ldo = n;
   a.out = out;

@@ -298,6 +298,36 @@ def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
             "timed_update": len(hist)}
 
 
+def update_gemm_roofline(dev, rows: int = 2097152, reps: int = 10) -> dict:
+    """The update's dominant kernel, the 512 -> 512 hidden-layer forward in fp32 arithmetic on the bf16
+    matrix cores (csrc/vss_gemm_x6.hip), at the update's minibatch size, timed with HIP events on its
+    launch stream.  Achieved = fp32 FLOP (2 rows K N) / launch time; peaks: the x6 form's (the dense bf16
+    MFMA rate / 6 products, MI355X_MICROARCH.md ~2.5 PF dense bf16) and the fp32 MFMA peak."""
+    from vss_amd.update import linear_tanh_x6
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.tanh(torch.randn(rows, 512, device=dev, generator=g))
+    w = torch.randn(512, 512, device=dev, generator=g) / 512 ** 0.5
+    b = torch.zeros(512, device=dev)
+    y = torch.empty(rows, 512, device=dev)
+    for _ in range(2):
+        linear_tanh_x6(x, w, b, out=y)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        linear_tanh_x6(x, w, b, out=y)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    tf = 2.0 * rows * 512 * 512 / (ms * 1e-3) / 1e12
+    peak_x6, peak_fp32 = 2500.0 / 6, 157.3
+    del x, y
+    torch.cuda.empty_cache()
+    return {"kernel": "vss_linear_tanh_bf16x6 512->512 (update forward, 2,097,152 rows)", "bound": "mfma",
+            "achieved": tf, "peak": peak_x6, "unit": "TFLOP/s (fp32 FLOP)", "frac": tf / peak_x6,
+            "fp32_mfma_peak": peak_fp32, "vs_fp32_mfma_peak": tf / peak_fp32, "kernel_ms": ms}
+
+
 def reduce_max(values, device="cpu"):
     """Max over ranks of the per-rank timings (the only cross-rank data besides barriers)."""
     t = torch.tensor(values, dtype=torch.float64, device=device)
@@ -444,6 +474,8 @@ def main():
         if world > 1:
             dist.barrier()
         ppo = ppo_wallclock(n, ppo_updates, dev, world)
+        if rank == 0:
+            ppo["update_gemm_roofline"] = update_gemm_roofline(dev)
 
     if rank == 0:
         agents = 3 if args.mode == "dma" else 1

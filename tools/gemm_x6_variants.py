@@ -80,6 +80,20 @@ def main():
         cases.append((f"WGRAD {n}x{k}", 2.0 * rows * k * n,
                       lambda lib, old, gg=gg, x=x, n=n, k=k: lib.vss_weight_grad_bf16x6(
                           st, rows, n, k, gg.data_ptr(), x.data_ptr(), part.data_ptr())))
+    # every variant's results bitwise against the product library's (same arithmetic, same order)
+    for name, _, fn in cases:
+        out.zero_()
+        part.zero_()
+        fn(L[0][1], L[0][2])
+        torch.cuda.synchronize()
+        ref = (out.clone(), part.clone())
+        for v, lib, old in L[1:]:
+            out.zero_()
+            part.zero_()
+            fn(lib, old)
+            torch.cuda.synchronize()
+            same = torch.equal(out, ref[0]) and torch.equal(part, ref[1])
+            print(f"check {name:14s} {v}: {'bit-exact' if same else 'DIFFERS'}", flush=True)
     # clocks up before the first measured case (the first case otherwise measures the ramp)
     for _ in range(3):
         for _, fn in [(c[0], c[2]) for c in cases]:

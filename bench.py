@@ -34,6 +34,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "rsoccer-isaac-cleanrl_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 
+# before torch initialises the GPU: the PPO leg's captured minibatch needs ROCm's graph packet capture
+# off (ppo_continuous_action_isaacgym.py UPDATE_GRAPH_SAFE)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402

@@ -27,6 +27,16 @@ import time
 import numpy as np
 import torch
 import torch.distributed as dist
+
+# The update's captured minibatch (MinibatchGraph) needs ROCm's graph packet capture off: with it on,
+# a captured 2,097,152-row minibatch replays wrongly from its 9th launch on, deterministically, with
+# or without a synchronize between launches. With it off, 32 replays are bit-exact with eager
+# (tools/graph_probe.py, profiles/r03w_graph_probe*.log).  The runtime reads the switch when it
+# initialises, so it is set here, before anything touches the GPU; otherwise the update runs eagerly.
+_PACKET_CAPTURE = "DEBUG_CLR_GRAPH_PACKET_CAPTURE"
+if _PACKET_CAPTURE not in os.environ and not torch.cuda.is_initialized():
+    os.environ[_PACKET_CAPTURE] = "0"
+UPDATE_GRAPH_SAFE = os.environ.get(_PACKET_CAPTURE) == "0"
 import torch.nn as nn
 import torch.optim as optim
 from torch.distributions.normal import Normal
@@ -97,6 +107,9 @@ def parse_args(argv=None):
                         "reference's single-process loop does (ppo…:324-326); off = per-rank statistics")
     p.add_argument("--amp", type=str, default="none", choices=["none", "bf16"],
                    help="bf16 autocast for the MLP GEMMs (off = the reference's fp32 numerics)")
+    p.add_argument("--update-graph", type=b, default=True, nargs="?", const=True,
+                   help="replay each minibatch's forward, losses and backward as one captured HIP graph "
+                        "(MinibatchGraph; on a ROCm GPU with --amp none), eager otherwise")
     args = p.parse_args(argv)
     args.batch_size = int(args.num_envs * args.num_steps)
     args.minibatch_size = int(args.batch_size // args.num_minibatches)
@@ -323,7 +336,9 @@ def get_action_and_value_update(agent: "Agent", x, action):
     the MLPs through _TanhMLP, split-K weight gradients in the backward."""
     mean = _mlp_forward(agent.actor_mean, x)
     std = torch.exp(agent.actor_logstd.expand_as(mean))
-    probs = Normal(mean, std)
+    # no argument validation: its finiteness check is a host sync per minibatch, which a captured
+    # minibatch (MinibatchGraph) cannot hold; the loss values are the same
+    probs = Normal(mean, std, validate_args=False)
     return action, probs.log_prob(action).sum(1), probs.entropy().sum(1), _mlp_forward(agent.critic, x)
 
 
@@ -505,43 +520,119 @@ def value_loss(newvalue, mb_returns, mb_values, clip_coef: float, clip_vloss: bo
     return 0.5 * ((newvalue - mb_returns) ** 2).mean()
 
 
+def minibatch_losses(agent, args, obs, actions, logprobs, adv, returns, values):
+    """The clipped PPO losses of ppo…:318-349 on one minibatch (adv already normalised when
+    --norm-adv): (loss, (pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac))."""
+    if getattr(args, "amp", "none") == "none":
+        _, newlogprob, entropy, newvalue = get_action_and_value_update(agent, obs, actions)
+    else:
+        with autocast(args, obs.device):
+            _, newlogprob, entropy, newvalue = agent.get_action_and_value(obs, actions)
+    newlogprob, entropy, newvalue = newlogprob.float(), entropy.float(), newvalue.float()
+    logratio = newlogprob - logprobs
+    ratio = logratio.exp()
+    with torch.no_grad():
+        old_approx_kl = (-logratio).mean()
+        approx_kl = ((ratio - 1) - logratio).mean()
+        clipfrac = ((ratio - 1.0).abs() > args.clip_coef).float().mean()
+    pg_loss = torch.max(-adv * ratio, -adv * torch.clamp(ratio, 1 - args.clip_coef, 1 + args.clip_coef)).mean()
+    v_loss = value_loss(newvalue.view(-1), returns, values, args.clip_coef, args.clip_vloss)
+    entropy_loss = entropy.mean()
+    loss = pg_loss - args.ent_coef * entropy_loss + v_loss * args.vf_coef
+    return loss, (pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac)
+
+
+class MinibatchGraph:
+    """One minibatch's forward, losses and backward (into FlatGrads) captured once as a HIP graph and
+    replayed for every minibatch: ~300 launches (the MLP GEMMs, the loss and its autograd ops, the
+    gradient zeroing) become one graph launch.  At the reference's 4,095 envs the update is launch-
+    bound -- 131,040-row minibatches, 12,000 launches per update, the GPU idle ~23 % of it
+    (profiles/r03w_trace_summary.txt).  The gathers into the static inputs, the advantage
+    normalisation (with its all-reduce when world > 1), the gradient all-reduce, clipping and the
+    Adam step run eagerly around the replay, so the optimizer is torch's own (host-side bias
+    corrections) and the learning-rate schedules apply unchanged.  The kernels and their order are
+    the eager path's, so the results are the same bits (tests/test_ppo.py)."""
+
+    def __init__(self, agent, flat, args, mb, obs_dim, act_dim, device):
+        self.agent, self.flat, self.args = agent, flat, args
+        z = lambda *shape: torch.zeros(shape, device=device)  # noqa: E731
+        self.obs, self.act = z(mb, *obs_dim), z(mb, *act_dim)
+        self.logp, self.adv, self.ret, self.val = z(mb), z(mb), z(mb), z(mb)
+        self.graph = None
+        self.out = None
+
+    def _body(self):
+        self.flat.zero()
+        loss, st = minibatch_losses(self.agent, self.args, self.obs, self.act, self.logp, self.adv, self.ret,
+                                    self.val)
+        loss.backward()
+        return st
+
+    def _capture(self):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up: library handles, workspaces, autograd caches
+            self._body()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        # the warm-up's blocks back to the device before the graph's private pool takes its own
+        # (a minibatch of DMA config 4 holds ~100 GB of activations and gradients)
+        torch.cuda.empty_cache()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.out = self._body()
+        self.graph = g
+
+    def run(self, inds, b_obs, b_actions, b_logprobs, mb_adv, b_returns, b_values):
+        torch.index_select(b_obs, 0, inds, out=self.obs)
+        torch.index_select(b_actions, 0, inds, out=self.act)
+        torch.index_select(b_logprobs, 0, inds, out=self.logp)
+        torch.index_select(b_returns, 0, inds, out=self.ret)
+        torch.index_select(b_values, 0, inds, out=self.val)
+        self.adv.copy_(mb_adv)
+        if self.graph is None:
+            self._capture()
+        self.graph.replay()
+        return self.out
+
+
+def make_minibatch_graph(agent, flat, args, batch, obs_dim, act_dim, device):
+    """MinibatchGraph when --update-graph applies (ROCm GPU, fp32, equal minibatches, graph packet
+    capture off), else None."""
+    mb = batch // args.num_minibatches
+    if not getattr(args, "update_graph", False) or torch.device(device).type != "cuda" or \
+            getattr(args, "amp", "none") != "none" or batch % mb or not UPDATE_GRAPH_SAFE:
+        return None
+    return MinibatchGraph(agent, flat, args, mb, obs_dim, act_dim, device)
+
+
 def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_advantages, b_returns,
-               b_values, world=1, gen=None):
+               b_values, world=1, gen=None, graph=None):
     """Clipped PPO over update_epochs x num_minibatches (ppo…:306-365).  Returns last-minibatch
-    stats.  `flat` holds the grads; with world > 1 it is all-reduced before clipping."""
+    stats.  `flat` holds the grads; with world > 1 it is all-reduced before clipping.  `graph` (a
+    MinibatchGraph) replays the minibatch's forward and backward; None runs them eagerly."""
     device = b_obs.device
     batch = b_obs.shape[0]
     mb = batch // args.num_minibatches
     clipfracs = []
-    stats = {}
     epochs_run = 0
     for epoch in range(args.update_epochs):
         epochs_run += 1
         b_inds = torch.randperm(batch, device=device, generator=gen)
         for start in range(0, batch, mb):
             mb_inds = b_inds[start:start + mb]
-            if getattr(args, "amp", "none") == "none":
-                _, newlogprob, entropy, newvalue = get_action_and_value_update(agent, b_obs[mb_inds], b_actions[mb_inds])
-            else:
-                with autocast(args, device):
-                    _, newlogprob, entropy, newvalue = agent.get_action_and_value(b_obs[mb_inds], b_actions[mb_inds])
-            newlogprob, entropy, newvalue = newlogprob.float(), entropy.float(), newvalue.float()
-            logratio = newlogprob - b_logprobs[mb_inds]
-            ratio = logratio.exp()
-            with torch.no_grad():
-                old_approx_kl = (-logratio).mean()
-                approx_kl = ((ratio - 1) - logratio).mean()
-                clipfracs.append(((ratio - 1.0).abs() > args.clip_coef).float().mean())
             mb_adv = b_advantages[mb_inds]
             if args.norm_adv:
                 mb_adv = normalize_advantages(mb_adv, world, getattr(args, "global_adv_norm", True))
-            pg_loss = torch.max(-mb_adv * ratio, -mb_adv * torch.clamp(ratio, 1 - args.clip_coef, 1 + args.clip_coef)).mean()
-            v_loss = value_loss(newvalue.view(-1), b_returns[mb_inds], b_values[mb_inds], args.clip_coef, args.clip_vloss)
-            entropy_loss = entropy.mean()
-            loss = pg_loss - args.ent_coef * entropy_loss + v_loss * args.vf_coef
-
-            flat.zero()
-            loss.backward()
+            if graph is not None:
+                st = graph.run(mb_inds, b_obs, b_actions, b_logprobs, mb_adv, b_returns, b_values)
+            else:
+                flat.zero()
+                loss, st = minibatch_losses(agent, args, b_obs[mb_inds], b_actions[mb_inds], b_logprobs[mb_inds],
+                                            mb_adv, b_returns[mb_inds], b_values[mb_inds])
+                loss.backward()
+            pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac = st
+            clipfracs.append(clipfrac.clone())  # (a graph's outputs are rewritten by the next replay)
             flat.all_reduce_mean(world)  # the data-parallel exchange (RCCL on ROCm)
             nn.utils.clip_grad_norm_(agent.parameters(), args.max_grad_norm)
             optimizer.step()
@@ -555,10 +646,9 @@ def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_adv
                                                              args.threshold_kl)
         if args.target_kl is not None and float(approx_kl) > args.target_kl:
             break
-    stats.update(v_loss=v_loss.detach(), pg_loss=pg_loss.detach(), entropy=entropy_loss.detach(),
-                 old_approx_kl=old_approx_kl, approx_kl=approx_kl,
-                 clipfrac=torch.stack(clipfracs).mean(), epochs_run=epochs_run)
-    return stats
+    return dict(v_loss=v_loss.detach().clone(), pg_loss=pg_loss.detach().clone(), entropy=entropy_loss.detach().clone(),
+                old_approx_kl=old_approx_kl.clone(), approx_kl=approx_kl.clone(),
+                clipfrac=torch.stack(clipfracs).mean(), epochs_run=epochs_run)
 
 
 def setup_distributed():
@@ -667,6 +757,7 @@ def train(args, on_update=None):
     values = torch.zeros((T, E), device=device)
     next_values = torch.zeros((T, E), device=device)
     term = TerminalValues(T, E, obs_dim, device) if fused is not None else None
+    graph = make_minibatch_graph(agent, flat, args, T * E, obs_dim, act_dim, device)
 
     global_step = 0
     start_time = time.time()
@@ -729,7 +820,7 @@ def train(args, on_update=None):
         t_upd = time.time()
         stats = ppo_update(agent, optimizer, flat, args, obs.reshape((-1,) + obs_dim), logprobs.reshape(-1),
                            actions.reshape((-1,) + act_dim), advantages.reshape(-1), returns.reshape(-1),
-                           values.reshape(-1), world=world, gen=gen)
+                           values.reshape(-1), world=world, gen=gen, graph=graph)
         if device.type == "cuda":
             torch.cuda.synchronize()
         t_upd = time.time() - t_upd

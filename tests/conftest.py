@@ -3,6 +3,10 @@ import sys
 
 import pytest
 
+# before any test initialises the GPU: the update's captured minibatch needs ROCm's graph packet
+# capture off (ppo_continuous_action_isaacgym.py UPDATE_GRAPH_SAFE)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "rsoccer-isaac-cleanrl_amd")
 for p in (PKG, os.path.join(REPO, "oracle"), REPO):

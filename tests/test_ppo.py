@@ -172,6 +172,43 @@ def test_data_parallel_update_gloo_world2(adv_norm):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,nmb,epochs,updates,norm_adv,clip_vloss", [
+    (2048, 2, 2, 2, True, True), (32768, 2, 2, 2, True, False), (32768, 2, 2, 2, False, True),
+    (8388608, 4, 3, 1, True, False)])
+def test_minibatch_graph_update_equals_eager_gpu(n, nmb, epochs, updates, norm_adv, clip_vloss):
+    """The captured minibatch step (MinibatchGraph) replays the eager step's kernels in the eager
+    order: the updates (Adam between the minibatches) end in the same parameter bits and the same
+    statistics.  n = 32,768: 16,384-row minibatches on the x6 GEMMs; n = 8,388,608: the config-3
+    minibatch (2,097,152 rows) replayed 12 times -- with graph packet capture on, the 9th replay
+    and every later one went wrong (profiles/r03w_graph_probe2.log)."""
+    args = _args(norm_adv=norm_adv, clip_vloss=clip_vloss, num_minibatches=nmb, update_epochs=epochs)
+    obs, act, logp, adv, ret, val = [t.cuda() for t in _synthetic_batch(5, n)]
+    res = []
+    for use_graph in (False, True):
+        agent = make_agent(2).cuda()
+        flat = P.FlatGrads(agent)
+        opt = torch.optim.Adam(agent.parameters(), lr=1e-3, eps=1e-5)
+        graph = P.make_minibatch_graph(agent, flat, args, n, (52,), (2,), "cuda") if use_graph else None
+        assert (graph is not None) == use_graph
+        gen = torch.Generator(device="cuda").manual_seed(7)
+        stats = [P.ppo_update(agent, opt, flat, args, obs, logp, act, adv, ret, val, gen=gen, graph=graph)
+                 for _ in range(updates)]
+        res.append((torch.cat([p.detach().reshape(-1) for p in agent.parameters()]), stats))
+    assert torch.equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert {k: float(v) for k, v in a.items()} == {k: float(v) for k, v in b.items()}
+
+
+def test_minibatch_graph_only_on_gpu_fp32_equal_minibatches():
+    agent = make_agent(2)
+    flat = P.FlatGrads(agent)
+    assert P.make_minibatch_graph(agent, flat, _args(), 256, (52,), (2,), "cpu") is None
+    assert P.make_minibatch_graph(agent, flat, _args(update_graph=False), 256, (52,), (2,), "cuda") is None
+    assert P.make_minibatch_graph(agent, flat, _args(amp="bf16"), 256, (52,), (2,), "cuda") is None
+    assert P.make_minibatch_graph(agent, flat, _args(), 257, (52,), (2,), "cuda") is None
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("env_id", ["sa", "cma", "dma"])
 def test_train_end_to_end_gpu(env_id, tmp_path):
     """Two PPO updates on the HIP env (small config): finite losses, rewards flow, SPS > 0."""

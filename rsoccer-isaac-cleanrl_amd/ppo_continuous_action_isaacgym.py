@@ -559,6 +559,7 @@ class MinibatchGraph:
         self.obs, self.act = z(mb, *obs_dim), z(mb, *act_dim)
         self.logp, self.adv, self.ret, self.val = z(mb), z(mb), z(mb), z(mb)
         self.graph = None
+        self.warm = False
         self.out = None
 
     def _body(self):
@@ -566,18 +567,17 @@ class MinibatchGraph:
         loss, st = minibatch_losses(self.agent, self.args, self.obs, self.act, self.logp, self.adv, self.ret,
                                     self.val)
         loss.backward()
-        return st
+        # detached: no autograd graph (and no AccumulateGrad node bound to this stream) outlives the step
+        return tuple(t.detach() for t in st)
 
     def _capture(self):
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):  # warm-up: library handles, workspaces, autograd caches
-            self._body()
-        torch.cuda.current_stream().wait_stream(side)
+        # the first minibatch ran eagerly (library handles, workspaces, lazy initialisation); release the
+        # eager pool's cached blocks only when the device could not hold a second copy of them beside
+        # the graph's private pool (a minibatch of DMA config 4 holds ~100 GB of activations and gradients)
         torch.cuda.synchronize()
-        # the warm-up's blocks back to the device before the graph's private pool takes its own
-        # (a minibatch of DMA config 4 holds ~100 GB of activations and gradients)
-        torch.cuda.empty_cache()
+        free, _ = torch.cuda.mem_get_info()
+        if free < 1.25 * (torch.cuda.memory_reserved() - torch.cuda.memory_allocated()):
+            torch.cuda.empty_cache()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.out = self._body()
@@ -591,6 +591,9 @@ class MinibatchGraph:
         torch.index_select(b_values, 0, inds, out=self.val)
         self.adv.copy_(mb_adv)
         if self.graph is None:
+            if not self.warm:  # the first minibatch: eager, real work
+                self.warm = True
+                return self._body()
             self._capture()
         self.graph.replay()
         return self.out

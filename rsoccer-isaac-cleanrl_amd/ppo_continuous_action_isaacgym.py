@@ -520,15 +520,24 @@ def value_loss(newvalue, mb_returns, mb_values, clip_coef: float, clip_vloss: bo
     return 0.5 * ((newvalue - mb_returns) ** 2).mean()
 
 
+# the update's minibatch rows are padded to a multiple of this (MLP_ROW_PAD) on the GPU, so that every
+# hidden-layer GEMM runs on whole x6 tiles: at 4,095 envs a 131,040-row minibatch otherwise leaves
+# 224-row tails that hipBLASLt runs on one or two workgroups (43-110 us each, ~21 ms per update)
+MLP_ROW_PAD = 256
+
+
 def minibatch_losses(agent, args, obs, actions, logprobs, adv, returns, values):
     """The clipped PPO losses of ppo…:318-349 on one minibatch (adv already normalised when
-    --norm-adv): (loss, (pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac))."""
+    --norm-adv): (loss, (pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac)).
+    obs / actions may carry padding rows beyond the minibatch's len(logprobs) (copies of its first
+    rows): the networks run over them, the losses do not see them, so their gradient is zero."""
     if getattr(args, "amp", "none") == "none":
         _, newlogprob, entropy, newvalue = get_action_and_value_update(agent, obs, actions)
     else:
         with autocast(args, obs.device):
             _, newlogprob, entropy, newvalue = agent.get_action_and_value(obs, actions)
-    newlogprob, entropy, newvalue = newlogprob.float(), entropy.float(), newvalue.float()
+    n = logprobs.shape[0]
+    newlogprob, entropy, newvalue = newlogprob[:n].float(), entropy[:n].float(), newvalue[:n].float()
     logratio = newlogprob - logprobs
     ratio = logratio.exp()
     with torch.no_grad():
@@ -556,7 +565,8 @@ class MinibatchGraph:
     def __init__(self, agent, flat, args, mb, obs_dim, act_dim, device):
         self.agent, self.flat, self.args = agent, flat, args
         z = lambda *shape: torch.zeros(shape, device=device)  # noqa: E731
-        self.obs, self.act = z(mb, *obs_dim), z(mb, *act_dim)
+        mb_pad = mb + padding_rows(mb, device)
+        self.obs, self.act = z(mb_pad, *obs_dim), z(mb_pad, *act_dim)
         self.logp, self.adv, self.ret, self.val = z(mb), z(mb), z(mb), z(mb)
         self.graph = None
         self.warm = False
@@ -583,9 +593,9 @@ class MinibatchGraph:
             self.out = self._body()
         self.graph = g
 
-    def run(self, inds, b_obs, b_actions, b_logprobs, mb_adv, b_returns, b_values):
-        torch.index_select(b_obs, 0, inds, out=self.obs)
-        torch.index_select(b_actions, 0, inds, out=self.act)
+    def run(self, inds, inds_pad, b_obs, b_actions, b_logprobs, mb_adv, b_returns, b_values):
+        torch.index_select(b_obs, 0, inds_pad, out=self.obs)
+        torch.index_select(b_actions, 0, inds_pad, out=self.act)
         torch.index_select(b_logprobs, 0, inds, out=self.logp)
         torch.index_select(b_returns, 0, inds, out=self.ret)
         torch.index_select(b_values, 0, inds, out=self.val)
@@ -597,6 +607,11 @@ class MinibatchGraph:
             self._capture()
         self.graph.replay()
         return self.out
+
+
+def padding_rows(mb: int, device) -> int:
+    """Rows the update adds to a minibatch of mb rows (MLP_ROW_PAD on a ROCm GPU, none on the CPU)."""
+    return (-mb) % MLP_ROW_PAD if torch.device(device).type == "cuda" else 0
 
 
 def make_minibatch_graph(agent, flat, args, batch, obs_dim, act_dim, device):
@@ -617,6 +632,7 @@ def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_adv
     device = b_obs.device
     batch = b_obs.shape[0]
     mb = batch // args.num_minibatches
+    pad = padding_rows(mb, device)
     clipfracs = []
     epochs_run = 0
     for epoch in range(args.update_epochs):
@@ -624,14 +640,18 @@ def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_adv
         b_inds = torch.randperm(batch, device=device, generator=gen)
         for start in range(0, batch, mb):
             mb_inds = b_inds[start:start + mb]
+            # the networks' rows: the minibatch, then its first rows again up to the padding
+            inds_pad = mb_inds
+            if pad and mb_inds.numel() == mb:
+                inds_pad = torch.cat([mb_inds, mb_inds.repeat(-(-pad // mb))[:pad]])
             mb_adv = b_advantages[mb_inds]
             if args.norm_adv:
                 mb_adv = normalize_advantages(mb_adv, world, getattr(args, "global_adv_norm", True))
             if graph is not None:
-                st = graph.run(mb_inds, b_obs, b_actions, b_logprobs, mb_adv, b_returns, b_values)
+                st = graph.run(mb_inds, inds_pad, b_obs, b_actions, b_logprobs, mb_adv, b_returns, b_values)
             else:
                 flat.zero()
-                loss, st = minibatch_losses(agent, args, b_obs[mb_inds], b_actions[mb_inds], b_logprobs[mb_inds],
+                loss, st = minibatch_losses(agent, args, b_obs[inds_pad], b_actions[inds_pad], b_logprobs[mb_inds],
                                             mb_adv, b_returns[mb_inds], b_values[mb_inds])
                 loss.backward()
             pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac = st

@@ -174,6 +174,7 @@ def test_data_parallel_update_gloo_world2(adv_norm):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,nmb,epochs,updates,norm_adv,clip_vloss", [
     (2048, 2, 2, 2, True, True), (32768, 2, 2, 2, True, False), (32768, 2, 2, 2, False, True),
+    (262080, 2, 2, 1, True, False),  # 131,040-row minibatches (4,095 envs): 32 padding rows
     (8388608, 4, 3, 1, True, False)])
 def test_minibatch_graph_update_equals_eager_gpu(n, nmb, epochs, updates, norm_adv, clip_vloss):
     """The captured minibatch step (MinibatchGraph) replays the eager step's kernels in the eager
@@ -197,6 +198,31 @@ def test_minibatch_graph_update_equals_eager_gpu(n, nmb, epochs, updates, norm_a
     assert torch.equal(res[0][0], res[1][0])
     for a, b in zip(res[0][1], res[1][1]):
         assert {k: float(v) for k, v in a.items()} == {k: float(v) for k, v in b.items()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2000, 262080])
+def test_padded_minibatch_update_matches_unpadded_gpu(n, monkeypatch):
+    """The update's minibatch rows padded to whole 256-row GEMM tiles (MLP_ROW_PAD; the padding rows
+    are copies the losses do not see) give the unpadded update's parameters within fp32 summation-
+    order rounding: the padding contributes nothing."""
+    args = _args(norm_adv=True, clip_vloss=True)
+    data = [t.cuda() for t in _synthetic_batch(9, n)]
+    res = []
+    for pad in (256, 1):
+        monkeypatch.setattr(P, "MLP_ROW_PAD", pad)
+        agent = make_agent(2).cuda()
+        flat = P.FlatGrads(agent)
+        opt = torch.optim.Adam(agent.parameters(), lr=1e-3, eps=1e-5)
+        P.ppo_update(agent, opt, flat, args, *[data[k] for k in (0, 2, 1, 3, 4, 5)],
+                     gen=torch.Generator(device="cuda").manual_seed(7))
+        res.append(torch.cat([p.detach().reshape(-1) for p in agent.parameters()]))
+    torch.testing.assert_close(res[0], res[1], rtol=1e-4, atol=1e-6)
+
+
+def test_padding_rows():
+    assert P.padding_rows(131040, "cuda") == 32 and P.padding_rows(2097152, "cuda") == 0
+    assert P.padding_rows(100, "cuda") == 156 and P.padding_rows(131040, "cpu") == 0
 
 
 def test_minibatch_graph_only_on_gpu_fp32_equal_minibatches():

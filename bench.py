@@ -293,6 +293,9 @@ def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
             "update_gemm": {"x6": "fp32 arithmetic on the bf16 matrix cores (exact 3-way bf16 split, six partial "
                                   "products, fp32 accumulation; csrc/vss_gemm_x6.hip)",
                             "fp32": "fp32 MFMA (csrc/vss_update.hip)"}.get(P.UPDATE_GEMM, P.UPDATE_GEMM),
+            "update_minibatch": ("one captured HIP graph per minibatch (forward, losses, backward), "
+                                 f"rows padded to {P.MLP_ROW_PAD}" if P.UPDATE_GRAPH_SAFE and args.update_graph
+                                 else "eager"),
             "gradient_exchange": ("one flat fp32 all-reduce per minibatch "
                                   f"({dist.get_backend() if dist.is_initialized() else 'none'})") if world > 1 else "none",
             "rollout_s": roll_s, "update_s": upd_s,

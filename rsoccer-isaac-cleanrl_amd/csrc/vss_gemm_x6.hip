@@ -37,6 +37,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/vss.h"
 
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
@@ -115,6 +117,12 @@ struct Cfg {
   static_assert(LDS <= 160 * 1024, "the LDS image must fit a CU");
 };
 using CfgA = Cfg<128, 256, 2, 4>;
+// forward / backward with n % 256 == 0 (every layer of the Agent): 256 features x 128 rows, 4 x 2
+// waves.  Against CfgA the activation tile each block stages through registers and splits is half
+// as large and is shared by half as many blocks (ni = n / 256), while the weight tile, twice as
+// large, still arrives by LDS-DMA: forward 8-10 %, backward 1-2 % faster, the same bits
+// (profiles/r03z_gemm_x6_fb256.log)
+using CfgB = Cfg<256, 128, 4, 2>;
 
 struct Args {
   int32_t ni, nj;          // i tiles, j tiles (of BI, BJ)
@@ -191,14 +199,15 @@ __device__ __forceinline__ void write_op(const u32x4 (*src)[2], char* img) {
 // (128 rows) and K tile kt, [plane][k group g][row r][8 bf16] of W[128 it + r][32 kt + 8 g + e] --
 // exactly the bytes of the GEMM's P image, so each wave copies its slice with global_load_lds_dwordx4
 // (1 KB per wave instruction, contiguous in global memory and LDS)
+template <int R>
 __global__ __launch_bounds__(256) void split_image_kernel(const float* __restrict__ w, int64_t n, int64_t k,
                                                           uint16_t* __restrict__ img) {
   const int64_t ktn = k / KT, units = n * k / 8;
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (it, kt, g, r), r fastest
   if (u >= units) return;
-  const int r = (int)(u % 128), g = (int)((u / 128) % 4);
-  const int64_t kt = (u / 512) % ktn, it = u / (512 * ktn);
-  const float* src = w + (it * 128 + r) * k + kt * KT + 8 * g;
+  const int r = (int)(u % R), g = (int)((u / R) % 4);
+  const int64_t kt = (u / (4 * R)) % ktn, it = u / (4 * R * ktn);
+  const float* src = w + (it * R + r) * k + kt * KT + 8 * g;
   const u32x4 a = *reinterpret_cast<const u32x4*>(src), b = *reinterpret_cast<const u32x4*>(src + 4);
   float v[8];
 #pragma unroll
@@ -208,10 +217,10 @@ __global__ __launch_bounds__(256) void split_image_kernel(const float* __restric
   }
   u32x4 hi, mid, lo;
   split8(v, hi, mid, lo);
-  uint16_t* d = img + (it * ktn + kt) * (3 * 4 * 128 * 8) + (g * 128 + r) * 8;
+  uint16_t* d = img + (it * ktn + kt) * (3 * 4 * R * 8) + (g * R + r) * 8;
   *reinterpret_cast<u32x4*>(d) = hi;
-  *reinterpret_cast<u32x4*>(d + 4 * 128 * 8) = mid;
-  *reinterpret_cast<u32x4*>(d + 2 * 4 * 128 * 8) = lo;
+  *reinterpret_cast<u32x4*>(d + 4 * R * 8) = mid;
+  *reinterpret_cast<u32x4*>(d + 2 * 4 * R * 8) = lo;
 }
 
 // sum over the 16 lanes of a DPP row (as vss_update.hip row16_sum)
@@ -234,7 +243,8 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
   // wave per K tile), only the activations go through registers
   constexpr bool PDMA = SP == ST_DMA;
   constexpr int PI = PDMA ? 0 : C::PI;
-  static_assert(!PDMA || (BI == 128 && Img<BI>::BYTES == (C::THREADS / 64) * 3 * 1024), "DMA slices: 3 KB per wave");
+  constexpr int NQ = Img<BI>::BYTES / (C::THREADS / 64) / 1024;  // 1-KB DMA slices per wave per K tile
+  static_assert(!PDMA || NQ * (C::THREADS / 64) * 1024 == Img<BI>::BYTES, "DMA slices: whole KB per wave");
   constexpr int EPI_FLOATS = EPI == EPI_TANH_OUT ? KO * 256 + BI : (EPI == EPI_WGRAD ? 1 : BI);
   // one LDS object (a second __shared__ array beside a global_load_lds target can make hipcc wait
   // vmcnt(0) before the k-steps' LDS reads, cdna_hip_programming.md §5)
@@ -309,8 +319,8 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     if constexpr (PDMA) {
       const int64_t off = ((int64_t)it0 * (2 * a.kpairs) + kt) * Img<BI>::BYTES;
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int slice = (wv * 3 + q) * 1024;
+      for (int q = 0; q < NQ; ++q) {
+        const int slice = (wv * NQ + q) * 1024;
         // (C-style casts: the builtin takes a global and an LDS address-space pointer)
         __builtin_amdgcn_global_load_lds(
             (__attribute__((address_space(1))) void*)(static_cast<const char*>(a.p) + off + slice + lane * 16),
@@ -488,23 +498,32 @@ struct Plan {
   int64_t kpairs;
 };
 
-// forward / backward: exact shapes only (the update's minibatches): rows % 256, n % 128, k % 64
+// forward / backward: exact shapes only (the update's minibatches): rows % BJ, n % BI, k % 64
+template <class C>
 static bool fb_shape_ok(int64_t rows, int32_t k, int32_t n) {
-  return rows > 0 && rows % CfgA::BJ == 0 && rows / CfgA::BJ <= (1 << 22) && n > 0 && n % CfgA::BI == 0 && n <= 4096 &&
-         k > 0 && k % (2 * KT) == 0 && k <= 65536 && (rows / CfgA::BJ) * (n / CfgA::BI) <= 0x3fffffff;
+  return rows > 0 && rows % C::BJ == 0 && rows / C::BJ <= (1 << 22) && n > 0 && n % C::BI == 0 && n <= 4096 &&
+         k > 0 && k % (2 * KT) == 0 && k <= 65536 && (rows / C::BJ) * (n / C::BI) <= 0x3fffffff;
 }
 
+template <class C>
 static Plan fb_plan(int64_t rows, int32_t k, int32_t n) {
   Plan p;
-  p.ni = n / CfgA::BI;
-  p.nj = (int32_t)(rows / CfgA::BJ);
+  p.ni = n / C::BI;
+  p.nj = (int32_t)(rows / C::BJ);
   p.kpairs = k / (2 * KT);
   p.splits = 1;
   p.items = p.ni * p.nj;
-  int g = kGridCus * CfgA::BPC;
+  int g = kGridCus * C::BPC;
   g -= g % (8 * p.ni);  // a fixed i tile per block, 8 XCD slots
   p.grid = (g > 0 && g < p.items) ? g : p.items;
   return p;
+}
+
+// the forward / backward block for n features: CfgB where n % 256 == 0, else CfgA (n % 128); the
+// host functions below take the chosen configuration as their first argument
+template <class F>
+static auto with_fb_cfg(int32_t n, F&& f) {
+  return n > 0 && n % CfgB::BI == 0 ? f(CfgB{}) : f(CfgA{});
 }
 
 // weight gradient: dW (n_out, k_in) = grad^T x over `rows`: k_in % 128, n_out % 256, rows % 64;
@@ -532,14 +551,14 @@ static Plan wg_plan(int64_t rows, int32_t n_out, int32_t k_in) {
   return p;
 }
 
-template <int EPI, int SP, int SQ, int KO = 0>
+template <int EPI, int SP, int SQ, class C, int KO = 0>
 static int launch(void* stream, Args a, const Plan& pl) {
   a.ni = pl.ni;
   a.nj = pl.nj;
   a.kpairs = pl.kpairs;
   a.items = pl.items;
   a.splits = pl.splits;
-  hipLaunchKernelGGL((gemm_x6_kernel<EPI, SP, SQ, CfgA, KO>), dim3((unsigned)pl.grid), dim3(CfgA::THREADS), 0,
+  hipLaunchKernelGGL((gemm_x6_kernel<EPI, SP, SQ, C, KO>), dim3((unsigned)pl.grid), dim3(C::THREADS), 0,
                      (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
@@ -548,10 +567,11 @@ static bool misaligned(const void* p) { return !p || (reinterpret_cast<uintptr_t
 
 // the weight operand's planes: w (n, k) fp32 -> w_split, the tile-ordered LDS images of its bf16
 // planes (3 n k uint16, split_image_kernel), which the GEMM copies with global_load_lds
+template <class C>
 static int split_weight(void* stream, const float* w, int64_t n, int64_t k, uint16_t* w_split) {
   const int64_t units = n * k / 8;
-  hipLaunchKernelGGL(split_image_kernel, dim3((unsigned)((units + 255) / 256)), dim3(256), 0, (hipStream_t)stream, w, n,
-                     k, w_split);
+  hipLaunchKernelGGL(split_image_kernel<C::BI>, dim3((unsigned)((units + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, w, n, k, w_split);
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 
@@ -574,54 +594,67 @@ extern "C" {
 int vss_linear_tanh_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
                            const float* bias, float* y, uint16_t* w_split) {
   using namespace vx6;
-  if (!fb_shape_ok(rows, k_in, n_out) || misaligned(x) || misaligned(w) || misaligned(y) || !bias || misaligned(w_split))
-    return VSS_E_ARG;
-  int rc = split_weight(stream, w, n_out, k_in, w_split);
-  if (rc != VSS_OK) return rc;
-  Args a = fb_args(k_in, n_out, w_split, x, y);
-  a.bias = bias;
-  return launch<EPI_TANH, ST_DMA, ST_ROW>(stream, a, fb_plan(rows, k_in, n_out));
+  return with_fb_cfg(n_out, [&](auto cfg) {
+    using C = decltype(cfg);
+    if (!fb_shape_ok<C>(rows, k_in, n_out) || misaligned(x) || misaligned(w) || misaligned(y) || !bias ||
+        misaligned(w_split))
+      return (int)VSS_E_ARG;
+    int rc = split_weight<C>(stream, w, n_out, k_in, w_split);
+    if (rc != VSS_OK) return rc;
+    Args a = fb_args(k_in, n_out, w_split, x, y);
+    a.bias = bias;
+    return launch<EPI_TANH, ST_DMA, ST_ROW, C>(stream, a, fb_plan<C>(rows, k_in, n_out));
+  });
 }
 
 int vss_linear_tanh_out_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
                                const float* bias, float* y, int32_t k_out, const float* w_out, float* out_part,
                                uint16_t* w_split) {
   using namespace vx6;
-  if (!fb_shape_ok(rows, k_in, n_out) || n_out != 256 || misaligned(x) || misaligned(w) || misaligned(y) || !bias ||
-      !w_out || !out_part || !(k_out == 1 || k_out == 2 || k_out == 6) || misaligned(w_split))
-    return VSS_E_ARG;
-  int rc = split_weight(stream, w, n_out, k_in, w_split);
-  if (rc != VSS_OK) return rc;
-  Args a = fb_args(k_in, n_out, w_split, x, y);
-  a.bias = bias;
-  a.w_out = w_out;
-  a.out_part = out_part;
-  const Plan pl = fb_plan(rows, k_in, n_out);
-  if (k_out == 1) return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, 1>(stream, a, pl);
-  if (k_out == 2) return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, 2>(stream, a, pl);
-  return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, 6>(stream, a, pl);
+  return with_fb_cfg(n_out, [&](auto cfg) {
+    using C = decltype(cfg);
+    if (!fb_shape_ok<C>(rows, k_in, n_out) || n_out != 256 || misaligned(x) || misaligned(w) || misaligned(y) ||
+        !bias || !w_out || !out_part || !(k_out == 1 || k_out == 2 || k_out == 6) || misaligned(w_split))
+      return (int)VSS_E_ARG;
+    int rc = split_weight<C>(stream, w, n_out, k_in, w_split);
+    if (rc != VSS_OK) return rc;
+    Args a = fb_args(k_in, n_out, w_split, x, y);
+    a.bias = bias;
+    a.w_out = w_out;
+    a.out_part = out_part;
+    const Plan pl = fb_plan<C>(rows, k_in, n_out);
+    if (k_out == 1) return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, C, 1>(stream, a, pl);
+    if (k_out == 2) return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, C, 2>(stream, a, pl);
+    return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, C, 6>(stream, a, pl);
+  });
 }
 
 int64_t vss_linear_tanh_backward_chunks_bf16x6(int64_t rows, int32_t k_next, int32_t n_out) {
   using namespace vx6;
-  if (!fb_shape_ok(rows, k_next, n_out)) return -1;
-  const Plan pl = fb_plan(rows, k_next, n_out);
-  return pl.grid / pl.ni;
+  return with_fb_cfg(n_out, [&](auto cfg) -> int64_t {
+    using C = decltype(cfg);
+    if (!fb_shape_ok<C>(rows, k_next, n_out)) return -1;
+    const Plan pl = fb_plan<C>(rows, k_next, n_out);
+    return pl.grid / pl.ni;
+  });
 }
 
 int vss_linear_tanh_backward_bf16x6(void* stream, int64_t rows, int32_t k_next, int32_t n_out, const float* grad_next,
                                     const float* w_next_t, const float* y, float* grad_in, float* bias_partial,
                                     uint16_t* w_split) {
   using namespace vx6;
-  if (!fb_shape_ok(rows, k_next, n_out) || misaligned(grad_next) || misaligned(w_next_t) || misaligned(y) ||
-      misaligned(grad_in) || misaligned(bias_partial) || misaligned(w_split))
-    return VSS_E_ARG;
-  int rc = split_weight(stream, w_next_t, n_out, k_next, w_split);
-  if (rc != VSS_OK) return rc;
-  Args a = fb_args(k_next, n_out, w_split, grad_next, grad_in);
-  a.y = y;
-  a.partial = bias_partial;
-  return launch<EPI_DTANH, ST_DMA, ST_ROW>(stream, a, fb_plan(rows, k_next, n_out));
+  return with_fb_cfg(n_out, [&](auto cfg) {
+    using C = decltype(cfg);
+    if (!fb_shape_ok<C>(rows, k_next, n_out) || misaligned(grad_next) || misaligned(w_next_t) || misaligned(y) ||
+        misaligned(grad_in) || misaligned(bias_partial) || misaligned(w_split))
+      return (int)VSS_E_ARG;
+    int rc = split_weight<C>(stream, w_next_t, n_out, k_next, w_split);
+    if (rc != VSS_OK) return rc;
+    Args a = fb_args(k_next, n_out, w_split, grad_next, grad_in);
+    a.y = y;
+    a.partial = bias_partial;
+    return launch<EPI_DTANH, ST_DMA, ST_ROW, C>(stream, a, fb_plan<C>(rows, k_next, n_out));
+  });
 }
 
 int64_t vss_weight_grad_chunks_bf16x6(int64_t rows, int32_t n_out, int32_t k_in) {
@@ -641,7 +674,7 @@ int vss_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_
   a.q = grad;
   a.ldo = k_in;
   a.out = partial;
-  return launch<EPI_WGRAD, ST_TR, ST_TR>(stream, a, wg_plan(rows, n_out, k_in));
+  return launch<EPI_WGRAD, ST_TR, ST_TR, CfgA>(stream, a, wg_plan(rows, n_out, k_in));
 }
 
 }  // extern "C"

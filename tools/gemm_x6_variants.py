@@ -92,8 +92,9 @@ def main():
             part.zero_()
             fn(lib, old)
             torch.cuda.synchronize()
-            same = torch.equal(out, ref[0]) and torch.equal(part, ref[1])
-            print(f"check {name:14s} {v}: {'bit-exact' if same else 'DIFFERS'}", flush=True)
+            o, q = torch.equal(out, ref[0]), torch.equal(part, ref[1])
+            print(f"check {name:14s} {v}: output {'bit-exact' if o else 'DIFFERS'}, partials "
+                  f"{'bit-exact' if q else 'differ (layout or order)'}", flush=True)
     # clocks up before the first measured case (the first case otherwise measures the ramp)
     for _ in range(3):
         for _, fn in [(c[0], c[2]) for c in cases]:

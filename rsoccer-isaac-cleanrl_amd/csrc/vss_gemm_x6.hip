@@ -416,6 +416,18 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     // epilogue straight from the accumulators: lane holds out[j][i .. i + 3] for
     // i = i0 + 16 ti + 4 fg, j = j0 + 16 tj + fr
     const int ib = it * BI + wi * C::WTI, jb = jt * BJ + wj * C::WTJ;
+    // EPI_DTANH: the other y row groups are all requested before the first group's work, so their
+    // latencies overlap one another and that work instead of adding up group by group (the K loop's
+    // registers are free here); backward 8-13 % faster than one load per group at its use would be
+    // without any y traffic (tools/x6_ablate.py noy, profiles/r03z_epi_ablate.log)
+    f32x4 yrest[EPI == EPI_DTANH ? TJ : 1][EPI == EPI_DTANH ? TI : 1];
+    if constexpr (EPI == EPI_DTANH) {
+#pragma unroll
+      for (int j = 1; j < TJ; ++j)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+          yrest[j][i] = *reinterpret_cast<const f32x4*>(a.y + ((int64_t)jb + 16 * j + fr) * a.ldo + ib + 16 * i + 4 * fg);
+    }
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int64_t jg = (int64_t)jb + 16 * j + fr;
@@ -443,7 +455,7 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
             }
           }
         } else if constexpr (EPI == EPI_DTANH) {
-          const f32x4 yv = j == 0 ? ypre[i] : *reinterpret_cast<const f32x4*>(a.y + jg * a.ldo + ig);
+          const f32x4 yv = j == 0 ? ypre[i] : yrest[j][i];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             v[r] = v[r] * fmaf(-yv[r], yv[r], 1.0f);

@@ -9,6 +9,9 @@
             upper bound of taking P's staging out of the K loop, e.g. by LDS-DMA)
   bigfirst  (correct results) the six products largest first (hi.hi, hi.mid, mid.hi, hi.lo,
             mid.mid, lo.hi): the first MFMAs of a K tile need only the hi planes' fragments
+  notanh    the forward epilogue adds the bias but skips the tanh (its VALU cost)
+  noy       the backward epilogue reuses the prefetched first y row group for every row group
+            (the cost of the epilogue's y loads)
   wab       (correct results) the staging write placed AFTER the barrier: per K tile,
             swrite(next) -> gload(next + 2) -> MFMAs -> barrier (guide T14 / G15)
 Usage: python tools/x6_ablate.py nosplit nobar noglobal nosplit+noglobal"""
@@ -68,6 +71,9 @@ PATCH = {
   gload(r1);  // K tile 1
   gload(r0);  // K tile 2
   __syncthreads();""")],
+    "notanh": [("v[r] = tanh_f32(v[r] + epi_lds[il + r]);", "v[r] = v[r] + epi_lds[il + r];")],
+    "noy": [("const f32x4 yv = j == 0 ? ypre[i] : *reinterpret_cast<const f32x4*>(a.y + jg * a.ldo + ig);",
+             "const f32x4 yv = ypre[i];")],
     "noglobal": [("""      gload(r1);
       mfma_tile(1);""", """      mfma_tile(1);"""), ("""      gload(r0);
     }""", """    }""")],

@@ -589,7 +589,9 @@ class MinibatchGraph:
         if free < 1.25 * (torch.cuda.memory_reserved() - torch.cuda.memory_allocated()):
             torch.cuda.empty_cache()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: with several ranks, RCCL's and the process group's own threads keep querying
+        # their streams and events while this thread captures (no collective is captured)
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self.out = self._body()
         self.graph = g
 

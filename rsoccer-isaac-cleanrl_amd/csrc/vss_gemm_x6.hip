@@ -45,6 +45,7 @@
 #error "vss_gemm_x6.hip targets gfx950 (CDNA4) only: v_mfma_f32_16x16x32_bf16, v_cvt_pk_bf16_f32"
 #endif
 
+
 namespace vx6 {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -56,6 +57,9 @@ enum { EPI_TANH = 0, EPI_DTANH = 1, EPI_TANH_OUT = 2, EPI_WGRAD = 3 };
 enum { ST_ROW = 0, ST_TR = 1, ST_DMA = 2 };
 
 constexpr int KT = 32;  // K tile = one v_mfma_f32_16x16x32_bf16 step
+// EPI_DTANH: y row groups requested at the item's last K-tile pair (the rest at the epilogue's start);
+// two groups there spill and run 2-5 % slower (profiles/r03z_gemm_x6_colsum.log)
+constexpr int kYPre = 1;
 
 // tanh as vss_update.hip's tanh_f32 (odd polynomial below 0.3, exp2 form above)
 __device__ __forceinline__ float tanh_f32(float z) {
@@ -245,7 +249,8 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
   constexpr int PI = PDMA ? 0 : C::PI;
   constexpr int NQ = Img<BI>::BYTES / (C::THREADS / 64) / 1024;  // 1-KB DMA slices per wave per K tile
   static_assert(!PDMA || NQ * (C::THREADS / 64) * 1024 == Img<BI>::BYTES, "DMA slices: whole KB per wave");
-  constexpr int EPI_FLOATS = EPI == EPI_TANH_OUT ? KO * 256 + BI : (EPI == EPI_WGRAD ? 1 : BI);
+  // EPI_DTANH: (WJ, BI) column sums, accumulated item by item
+  constexpr int EPI_FLOATS = EPI == EPI_TANH_OUT ? KO * 256 + BI : (EPI == EPI_WGRAD ? 1 : (EPI == EPI_DTANH ? C::WJ * BI : BI));
   // one LDS object (a second __shared__ array beside a global_load_lds target can make hipcc wait
   // vmcnt(0) before the k-steps' LDS reads, cdna_hip_programming.md §5)
   __shared__ __attribute__((aligned(16))) char lds[C::LDS + EPI_FLOATS * 4];
@@ -268,7 +273,8 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
   int it0, jt0, sp0;
   item_ij(slot, it0, jt0, sp0);
   if constexpr (EPI != EPI_WGRAD) {
-    for (int i = tid; i < BI; i += C::THREADS) epi_lds[i] = EPI == EPI_DTANH ? 0.f : a.bias[it0 * BI + i];
+    for (int i = tid; i < (EPI == EPI_DTANH ? EPI_FLOATS : BI); i += C::THREADS)
+      epi_lds[i] = EPI == EPI_DTANH ? 0.f : a.bias[it0 * BI + i];
     if constexpr (EPI == EPI_TANH_OUT)
       for (int i = tid; i < KO * 256; i += C::THREADS) epi_lds[BI + i] = a.w_out[i];
   }
@@ -363,11 +369,6 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
                                                               __builtin_bit_cast(bf16x8, qf[QP[x]][j]), acc[i][j], 0, 0, 0);
   };
 
-  // EPI_DTANH: this lane's column sums, features wi*64 + 16 i + 4 fg + r, over all its tiles
-  float csum[EPI == EPI_DTANH ? TI : 1][4];
-#pragma unroll
-  for (int i = 0; i < (EPI == EPI_DTANH ? TI : 1); ++i) csum[i][0] = csum[i][1] = csum[i][2] = csum[i][3] = 0.f;
-
   Stage<PI + PJ> r0, r1;
   gload(r0);  // K tile 0
   dma_p(0, 0);
@@ -389,15 +390,18 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     // K-tile pair, so its HBM latency hides behind that pair's MFMAs instead of stalling the epilogue
     // (a y load issued in the epilogue also waits, by vmcnt's in-order count, for the next item's
     // prefetched K tiles)
-    f32x4 ypre[EPI == EPI_DTANH ? TI : 1];
+    f32x4 ypre[EPI == EPI_DTANH ? kYPre : 1][EPI == EPI_DTANH ? TI : 1];
     const int64_t jy = (int64_t)jt * BJ + wj * C::WTJ + fr;
     const int kn = (int)(kt_lo(sp + 1) - kt_lo(sp));  // this item's K tiles (even)
     for (int kt = 0; kt < kn; kt += 2) {
       if constexpr (EPI == EPI_DTANH) {
         if (kt + 2 >= kn) {
 #pragma unroll
-          for (int i = 0; i < TI; ++i)
-            ypre[i] = *reinterpret_cast<const f32x4*>(a.y + jy * a.ldo + it * BI + wi * C::WTI + 16 * i + 4 * fg);
+          for (int j = 0; j < kYPre; ++j)
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+              ypre[j][i] = *reinterpret_cast<const f32x4*>(a.y + (jy + 16 * j) * a.ldo + it * BI + wi * C::WTI + 16 * i +
+                                                           4 * fg);
         }
       }
       mfma_tile(0, [&] { dma_p(kt + 1, 1); });
@@ -415,6 +419,10 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
 
     // epilogue straight from the accumulators: lane holds out[j][i .. i + 3] for
     // i = i0 + 16 ti + 4 fg, j = j0 + 16 tj + fr
+    // EPI_DTANH: this item's column sums of the lane's features (16 i + 4 fg + r), over its rows
+    float cs[EPI == EPI_DTANH ? TI : 1][4];
+#pragma unroll
+    for (int i = 0; i < (EPI == EPI_DTANH ? TI : 1); ++i) cs[i][0] = cs[i][1] = cs[i][2] = cs[i][3] = 0.f;
     const int ib = it * BI + wi * C::WTI, jb = jt * BJ + wj * C::WTJ;
     // EPI_DTANH: the other y row groups are all requested before the first group's work, so their
     // latencies overlap one another and that work instead of adding up group by group (the K loop's
@@ -423,7 +431,7 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     f32x4 yrest[EPI == EPI_DTANH ? TJ : 1][EPI == EPI_DTANH ? TI : 1];
     if constexpr (EPI == EPI_DTANH) {
 #pragma unroll
-      for (int j = 1; j < TJ; ++j)
+      for (int j = kYPre; j < TJ; ++j)
 #pragma unroll
         for (int i = 0; i < TI; ++i)
           yrest[j][i] = *reinterpret_cast<const f32x4*>(a.y + ((int64_t)jb + 16 * j + fr) * a.ldo + ib + 16 * i + 4 * fg);
@@ -455,11 +463,11 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
             }
           }
         } else if constexpr (EPI == EPI_DTANH) {
-          const f32x4 yv = j == 0 ? ypre[i] : yrest[j][i];
+          const f32x4 yv = j < kYPre ? ypre[j < kYPre ? j : 0][i] : yrest[j][i];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             v[r] = v[r] * fmaf(-yv[r], yv[r], 1.0f);
-            csum[i][r] += v[r];
+            cs[i][r] += v[r];
           }
           __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig));
         } else {  // EPI_WGRAD: the split's partial
@@ -477,28 +485,29 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
         }
       }
     }
+    if constexpr (EPI == EPI_DTANH) {
+      // the 16 rows (lanes fr) of each k group, added to the wave's (wj, feature) slot: one lane
+      // per slot, so no two lanes ever add into the same word
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t = row16_sum(cs[i][r]);
+          if (fr == 0) epi_lds[wj * BI + wi * C::WTI + 16 * i + 4 * fg + r] += t;
+        }
+    }
     if (!has_next) break;
     w = next;
   }
 
   if constexpr (EPI == EPI_DTANH) {
-    // column sums: the 16 lanes (rows) of each k group, then the WJ waves of a feature slice in a
-    // fixed order (deterministic); partial[slot / ni][feature]
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(lds);  // (WJ, BI)
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float s = row16_sum(csum[i][r]);
-        if (fr == 0) red[wj * BI + wi * C::WTI + 16 * i + 4 * fg + r] = s;
-      }
+    // the WJ waves of a feature slice in a fixed order (deterministic); partial[slot / ni][feature]
     __syncthreads();
     for (int f = tid; f < BI; f += C::THREADS) {
-      float s = red[f];
+      float t = epi_lds[f];
 #pragma unroll
-      for (int m = 1; m < C::WJ; ++m) s += red[m * BI + f];
-      a.partial[(int64_t)(slot / a.ni) * (a.ni * BI) + it0 * BI + f] = s;
+      for (int m = 1; m < C::WJ; ++m) t += epi_lds[m * BI + f];
+      a.partial[(int64_t)(slot / a.ni) * (a.ni * BI) + it0 * BI + f] = t;
     }
   }
 }

@@ -54,7 +54,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 enum { EPI_TANH = 0, EPI_DTANH = 1, EPI_TANH_OUT = 2, EPI_WGRAD = 3 };
-enum { ST_ROW = 0, ST_TR = 1, ST_DMA = 2 };
+enum { ST_ROW = 0, ST_TR = 1, ST_DMA = 2, ST_TR2 = 3 };
 
 constexpr int KT = 32;  // K tile = one v_mfma_f32_16x16x32_bf16 step
 // EPI_DTANH: y row groups requested at the item's last K-tile pair (the rest at the epilogue's start);
@@ -156,6 +156,21 @@ struct Stage {
 template <int MODE, int R, int NP, class C>
 __device__ __forceinline__ void load_op(u32x4 (*dst)[2], const void* base_, int64_t ld, int64_t k0) {
   const int t = threadIdx.x;
+  if constexpr (MODE == ST_TR2) {
+    // ST_TR with two adjacent columns (image rows) per lane: one 8-B load per contraction row, half
+    // the load instructions for the same bytes (a wave reads 512 contiguous bytes of a row); weight
+    // gradient 1-2 % faster (profiles/r03zz_gemm_x6_tr2.log)
+    static_assert(NP == 2 && (R / 2) * 4 == C::THREADS, "ST_TR2: one column pair x 4 k groups per thread");
+    const int c2 = t % (R / 2), g = t / (R / 2);
+    const float* src = static_cast<const float*>(base_) + (k0 + 8 * g) * ld + 2 * c2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float2 x = *reinterpret_cast<const float2*>(src + e * ld);
+      dst[0][e >> 2][e & 3] = __float_as_uint(x.x);
+      dst[1][e >> 2][e & 3] = __float_as_uint(x.y);
+    }
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < NP; ++u) {
     const int pr = t + C::THREADS * u;
@@ -183,6 +198,12 @@ __device__ __forceinline__ void write_op(const u32x4 (*src)[2], char* img) {
     if constexpr (MODE == ST_TR) {
       row = pr % R;
       g = pr / R;
+    } else if constexpr (MODE == ST_TR2) {
+      // the lane's column pair: image rows 2 c2 and 2 c2 + 1.  An 8-lane write group then covers
+      // 4 row residues mod 8 (a 2-way bank conflict); swapping the pair's order in half the lanes
+      // removes it but its selects cost more than the conflict (1-3 % slower, r03zz_gemm_x6_tr2.log)
+      row = 2 * (t % (R / 2)) + u;
+      g = t / (R / 2);
     } else {
       g = (pr >> 3) & 3;  // lanes 8 q .. 8 q + 7: 8 consecutive rows of one group (one write lane group)
       row = (pr & 7) | ((pr >> 5) << 3);
@@ -297,7 +318,7 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     f_kn = (int)(kt_lo(sp + 1) - kt_lo(sp));
     if constexpr (SP == ST_TR) fp = static_cast<const char*>(a.p) + (int64_t)it * BI * 4;
     else fp = static_cast<const char*>(a.p);  // ST_DMA: addressed by dma_p
-    if constexpr (SQ == ST_TR) fq = reinterpret_cast<const char*>(a.q) + (int64_t)jt * BJ * 4;
+    if constexpr (SQ == ST_TR || SQ == ST_TR2) fq = reinterpret_cast<const char*>(a.q) + (int64_t)jt * BJ * 4;
     else fq = reinterpret_cast<const char*>(a.q) + (int64_t)jt * BJ * a.ldq * 4;
   };
   point(f_item);
@@ -695,7 +716,7 @@ int vss_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_
   a.q = grad;
   a.ldo = k_in;
   a.out = partial;
-  return launch<EPI_WGRAD, ST_TR, ST_TR, CfgA>(stream, a, wg_plan(rows, n_out, k_in));
+  return launch<EPI_WGRAD, ST_TR, ST_TR2, CfgA>(stream, a, wg_plan(rows, n_out, k_in));
 }
 
 }  // extern "C"

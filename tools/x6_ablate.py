@@ -5,6 +5,7 @@ tools/gemm_x6_variants.py:
   nosplit   the activations' staging writes store the raw fp32 words as planes (no split VALU)
   noglobal  the K loop issues no activation loads (the staged registers are written again as they are)
   qsmall    every item reads the Q rows of j tile 0 (L2-resident activations)
+  l2k       every K loop cycles over its first 4 K tiles (the staged operands L2-resident)
   bigfirst  (correct results) the six products largest first
   notanh    the forward epilogue adds the bias but skips the tanh (its VALU cost)
   noy       the backward epilogue reuses the prefetched first y row group for every row group
@@ -26,6 +27,7 @@ PATCH = {
     "bigfirst": [("""    constexpr int PP[6] = {2, 0, 1, 1, 0, 0};
     constexpr int QP[6] = {0, 2, 1, 0, 1, 0};""", """    constexpr int PP[6] = {0, 0, 1, 0, 1, 2};
     constexpr int QP[6] = {0, 1, 0, 2, 1, 0};""")],
+    "l2k": [("const int64_t k0 = fk0 + (int64_t)f_kt * KT;", "const int64_t k0 = fk0 + (int64_t)(f_kt & 3) * KT;")],
     "notanh": [("v[r] = tanh_f32(v[r] + epi_lds[il + r]);", "v[r] = v[r] + epi_lds[il + r];")],
     "noy": [("yrest[j][i] = *reinterpret_cast<const f32x4*>(a.y + ((int64_t)jb + 16 * j + fr) * a.ldo + ib + 16 * i + 4 * fg);",
              "yrest[j][i] = ypre[0][i];")],

@@ -596,6 +596,11 @@ class MinibatchGraph:
         self.graph = g
 
     def run(self, inds, inds_pad, b_obs, b_actions, b_logprobs, mb_adv, b_returns, b_values):
+        if inds.numel() != self.logp.numel() or inds_pad.numel() != self.obs.shape[0] or \
+                b_obs.shape[1:] != self.obs.shape[1:] or b_actions.shape[1:] != self.act.shape[1:]:
+            raise ValueError(f"MinibatchGraph: minibatch {inds.numel()} (+{inds_pad.numel() - inds.numel()} padding) "
+                             f"x {tuple(b_obs.shape[1:])} does not match the captured "
+                             f"{self.logp.numel()} (+{self.obs.shape[0] - self.logp.numel()}) x {tuple(self.obs.shape[1:])}")
         torch.index_select(b_obs, 0, inds_pad, out=self.obs)
         torch.index_select(b_actions, 0, inds_pad, out=self.act)
         torch.index_select(b_logprobs, 0, inds, out=self.logp)

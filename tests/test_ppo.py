@@ -220,6 +220,17 @@ def test_padded_minibatch_update_matches_unpadded_gpu(n, monkeypatch):
     torch.testing.assert_close(res[0], res[1], rtol=1e-4, atol=1e-6)
 
 
+def test_minibatch_graph_refuses_other_shapes():
+    """run() checks the minibatch against the captured static buffers before touching them (a CPU
+    stand-in object: no capture happens before the check)."""
+    g = P.MinibatchGraph.__new__(P.MinibatchGraph)
+    g.obs, g.act, g.logp = torch.zeros(256, 52), torch.zeros(256, 2), torch.zeros(200)
+    with pytest.raises(ValueError, match="does not match"):
+        g.run(torch.arange(100), torch.arange(256), torch.zeros(10, 52), torch.zeros(10, 2), None, None, None, None)
+    with pytest.raises(ValueError, match="does not match"):
+        g.run(torch.arange(200), torch.arange(256), torch.zeros(10, 51), torch.zeros(10, 2), None, None, None, None)
+
+
 def test_padding_rows():
     assert P.padding_rows(131040, "cuda") == 32 and P.padding_rows(2097152, "cuda") == 0
     assert P.padding_rows(100, "cuda") == 156 and P.padding_rows(131040, "cpu") == 0

@@ -24,6 +24,7 @@ csrc/vss_step.hip (source hash), else null.
 from __future__ import annotations
 
 import argparse
+import gc
 import hashlib
 import json
 import os
@@ -70,9 +71,12 @@ def parse():
     p.add_argument("--rollout-k", type=int, default=16,
                    help="also time vss_rollout with K steps per launch (0 = skip)")
     p.add_argument("--ppo-updates", type=int, default=None,
-                   help="PPO training updates run after the env-step benchmark, on every rank; the last one is "
-                        "timed (default 3: in this process the second update still carries warm-up, 4.2 s vs "
-                        "3.6 s steady state)")
+                   help="PPO-SA training updates run after the env-step benchmark, on every rank (default: until "
+                        "1e8 env-steps, 12 at 65,536 envs on one GPU; the train clock at 1e8 is the metric's "
+                        "second half; 0 = skip)")
+    p.add_argument("--ppo-dma-updates", type=int, default=2,
+                   help="PPO-DMA updates at the same fields per GPU (3 agent rows per field, BASELINE config 4); "
+                        "the last one is timed (0 = skip)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL) for real multi-GPU runs; gloo + --share-gpu to rehearse ranks on one GPU")
     p.add_argument("--share-gpu", action="store_true", help="map every rank to cuda:0 (rehearsal only)")
@@ -206,37 +210,53 @@ def past_l3_leg(n: int, steps: int, dev) -> dict:
             "env_steps_per_s": n / (ms * 1e-3)}
 
 
-def rollout_leg(env, K: int, steps: int, gen, dev) -> dict:
+def rollout_leg(env, K: int, steps: int, gen, dev, allocations: int = 6) -> dict:
     """vss_rollout: K FULL steps per launch for a pre-supplied random action sequence (the
     open-loop form of the same workload; state on chip between steps).  Bytes per field-step:
     actions 48 + obs 1248 + terminal obs 1248 + rew 96 + done 8 + time-out 1 + progress 4, plus
-    the state / bookkeeping / dof read+write (456 B) once per launch."""
+    the state / bookkeeping / dof read+write (456 B) once per launch.
+
+    The launch time depends on the physical pages behind the K-step output streams (DESIGN §5.1:
+    30.5-34.3 us per step over fresh allocations, reproducible within one), so the launches are
+    timed on `allocations` output buffers held at the same time (distinct pages) and the line reports
+    the MEDIAN allocation, with the spread beside it."""
     n = env.num_fields
     # episodes desynchronised (progress uniform over the episode length, as in a running training
     # loop) rather than all at the progress the FULL leg left; the progress distribution was measured
     # not to move this figure (profiles/r02_rollout_progress_distribution.log)
     env.progress_buf.random_(0, int(env.max_episode_length), generator=gen)
     acts = torch.rand((K, n, 2, 3, 2), device=dev, generator=gen) * 2 - 1
-    out = env.rollout(acts)
-    env.rollout(acts, out)
-    torch.cuda.synchronize()
+    outs = [env.rollout(acts) for _ in range(allocations)]
     launches = max(1, steps // K)
+    per_alloc_ms, walls = [], []
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record()
-    for _ in range(launches):
+    for out in outs:
         env.rollout(acts, out)
-    e1.record()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    launch_ms = e0.elapsed_time(e1) / launches
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0.record()
+        for _ in range(launches):
+            env.rollout(acts, out)
+        e1.record()
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t0)
+        per_alloc_ms.append(e0.elapsed_time(e1) / launches)
+    del outs
+    torch.cuda.empty_cache()
+    order = sorted(range(allocations), key=lambda i: per_alloc_ms[i])
+    med = order[allocations // 2]
+    launch_ms = per_alloc_ms[med]
     per_step_bytes = 48 + 1248 + 1248 + 96 + 8 + 1 + 4
     algo = n * (K * per_step_bytes + 368 + 32 + 8 + 48)
     achieved = algo / (launch_ms * 1e-3)
-    return {"steps_per_launch": K, "launches": launches, "value": n * K * launches / wall, "unit": "env-steps/s",
+    fr = [algo / (ms * 1e-3) / HBM_PEAK for ms in per_alloc_ms]
+    return {"steps_per_launch": K, "launches": launches, "value": n * K * launches / walls[med], "unit": "env-steps/s",
             "ms_per_step": launch_ms / K,
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": algo, "kernel_ms": launch_ms}}
+                         "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": algo, "kernel_ms": launch_ms,
+                         "allocations": allocations, "statistic": "median over the output allocations",
+                         "frac_min": min(fr), "frac_max": max(fr),
+                         "ms_per_step_each_allocation": [round(ms / K, 5) for ms in per_alloc_ms]}}
 
 
 def sa_leg(env, steps: int, gen, dev) -> dict:
@@ -269,24 +289,37 @@ def sa_leg(env, steps: int, gen, dev) -> dict:
                          "frac": achieved / HBM_PEAK, "algorithmic_bytes_per_launch": algo, "kernel_ms": ms}}
 
 
+def ppo_updates_to_1e8(n_envs: int, world: int, num_steps: int = 128) -> int:
+    """Updates until the global step count reaches 1e8 (ceil; the reference's total_timesteps //
+    batch_size with --total-timesteps 1e8 stops one update short of it)."""
+    import math
+    return math.ceil(1e8 / (n_envs * num_steps * world))
+
+
 def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
     """The full SA PPO loop (ppo_continuous_action_isaacgym.py, reference defaults: T=128,
-    8 epochs x 4 minibatches, fp32) at `n_envs` envs per rank; the last update is timed and
-    projected to 1e8 env-steps (ceil(1e8 / global batch) updates; the reference's floor-division
-    gives one fewer).  Runs on EVERY rank: at N > 1 each rank owns its own `n_envs` fields and
-    the gradients are averaged by one flat all-reduce per minibatch (RCCL), so the figures here
-    are max-over-ranks times and whole-job (all-rank) env-steps."""
-    import math
+    8 epochs x 4 minibatches, fp32) at `n_envs` envs per rank, for `updates` updates (by default
+    until 1e8 env-steps: 12 at 65,536 envs on one GPU).  `wallclock_to_1e8_steps_s` is MEASURED: the
+    train loop's own clock (ppo…:244, start before envs.reset()) at the end of the first update whose
+    global step reaches 1e8; the last update's rollout + update times projected to 1e8 are kept as
+    `projected_*`.  Runs on EVERY rank: at N > 1 each rank owns its own `n_envs` fields and the
+    gradients are averaged by one flat all-reduce per minibatch (RCCL), so the figures here are
+    max-over-ranks times and whole-job (all-rank) env-steps."""
     import ppo_continuous_action_isaacgym as P
     args = P.parse_args(["--env-id", "sa", "--num-envs", str(n_envs), "--num-updates", str(updates),
                          "--log", "false", "--seed", "1"])
+    t0 = time.perf_counter()
     _, hist = P.train(args)
+    call_s = time.perf_counter() - t0
     last = hist[-1]
-    roll_s, upd_s = reduce_max([last["rollout_s"], last["update_s"]],
-                               dev if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu")
+    red = dev if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu"
+    roll_s, upd_s, call_s = reduce_max([last["rollout_s"], last["update_s"], call_s], red)
+    walls = reduce_max([h["wall_s"] for h in hist], red)
     per_update = roll_s + upd_s
     batch = args.batch_size * world
-    updates_1e8 = math.ceil(1e8 / batch)
+    updates_1e8 = ppo_updates_to_1e8(n_envs, world, args.num_steps)
+    reached = next((i for i, h in enumerate(hist) if h["global_step"] >= 1e8), None)
+    ref_updates = int(1e8) // batch  # the reference's num_updates for --total-timesteps 1e8 (ppo…:247)
     return {"env": "sa", "n_gpus": world, "num_envs": n_envs * world, "num_envs_per_gpu": n_envs,
             "num_steps": args.num_steps, "batch": batch, "update_epochs": args.update_epochs,
             "num_minibatches": args.num_minibatches, "dtype": "f32",
@@ -298,10 +331,37 @@ def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
                                  else "eager"),
             "gradient_exchange": ("one flat fp32 all-reduce per minibatch "
                                   f"({dist.get_backend() if dist.is_initialized() else 'none'})") if world > 1 else "none",
-            "rollout_s": roll_s, "update_s": upd_s,
+            "updates_run": len(hist), "env_steps_run": hist[-1]["global_step"],
+            "wallclock_to_1e8_steps_s": walls[reached] if reached is not None else None,
+            "wallclock_to_1e8_steps": ("measured: train() clock at the end of update "
+                                       f"{reached + 1} ({hist[reached]['global_step']} env-steps)")
+            if reached is not None else f"not reached in {len(hist)} updates (see projected_wallclock_to_1e8_steps_s)",
+            "wallclock_reference_num_updates_s": walls[ref_updates - 1] if 0 < ref_updates <= len(hist) else None,
+            "reference_num_updates": ref_updates,
+            "wall_s_per_update": walls, "train_call_s": call_s,
+            "rollout_s": roll_s, "update_s": upd_s, "timed_update": len(hist),
             "rollout_env_steps_per_s": batch / roll_s, "train_env_steps_per_s": batch / per_update,
-            "wallclock_to_1e8_steps_s": updates_1e8 * per_update, "updates_to_1e8": updates_1e8,
-            "timed_update": len(hist)}
+            "projected_wallclock_to_1e8_steps_s": updates_1e8 * per_update, "updates_to_1e8": updates_1e8}
+
+
+def ppo_dma_leg(n_fields: int, updates: int, dev, world: int = 1) -> dict:
+    """BASELINE config 4: PPO-DMA (decentralised: every blue robot one agent row, envs/wrappers.py:
+    150-180) at `n_fields` fields per rank = 3 x n_fields agent rows, reference defaults; the last
+    update's rollout and update times (max over ranks)."""
+    import ppo_continuous_action_isaacgym as P
+    args = P.parse_args(["--env-id", "dma", "--num-envs", str(3 * n_fields), "--num-updates", str(updates),
+                         "--log", "false", "--seed", "1"])
+    _, hist = P.train(args)
+    last = hist[-1]
+    red = dev if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu"
+    roll_s, upd_s = reduce_max([last["rollout_s"], last["update_s"]], red)
+    rows = args.num_envs * world
+    return {"env": "dma", "n_gpus": world, "fields_per_gpu": n_fields, "agent_rows": rows,
+            "num_steps": args.num_steps, "batch": args.batch_size * world, "minibatch_rows": args.minibatch_size,
+            "updates_run": len(hist), "rollout_s": roll_s, "update_s": upd_s,
+            "rollout_agent_steps_per_s": rows * args.num_steps / roll_s,
+            "train_agent_steps_per_s": rows * args.num_steps / (roll_s + upd_s),
+            "mean_return_last": last["mean_return"], "v_loss_last": last["v_loss"], "entropy_last": last["entropy"]}
 
 
 def update_gemm_roofline(dev, rows: int = 2097152, reps: int = 10) -> dict:
@@ -472,16 +532,24 @@ def main():
 
     # ---- the PPO train loop on every rank (its gradient all-reduce is the one real exchange
     # step of the path); after the env-step timing, before the rank-0-only legs ----
-    ppo = None
-    ppo_updates = args.ppo_updates if args.ppo_updates is not None else 3
+    ppo = ppo_dma = None
+    ppo_updates = args.ppo_updates if args.ppo_updates is not None else ppo_updates_to_1e8(n, world)
+    if args.share_gpu:
+        os.environ["VSS_LOCAL_DEVICE"] = "0"
     if ppo_updates > 0:
-        if args.share_gpu:
-            os.environ["VSS_LOCAL_DEVICE"] = "0"
         if world > 1:
             dist.barrier()
         ppo = ppo_wallclock(n, ppo_updates, dev, world)
+        gc.collect()
+        torch.cuda.empty_cache()
         if rank == 0:
             ppo["update_gemm_roofline"] = update_gemm_roofline(dev)
+    if args.ppo_dma_updates > 0:
+        if world > 1:
+            dist.barrier()
+        ppo_dma = ppo_dma_leg(n, args.ppo_dma_updates, dev, world)
+        gc.collect()
+        torch.cuda.empty_cache()
 
     if rank == 0:
         agents = 3 if args.mode == "dma" else 1
@@ -535,6 +603,8 @@ def main():
             out["sa_step"] = sa_leg(env, args.steps, gen, dev)
         if ppo is not None:
             out["ppo"] = ppo
+        if ppo_dma is not None:
+            out["ppo_dma"] = ppo_dma
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(out), flush=True)

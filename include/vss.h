@@ -361,6 +361,30 @@ int vss_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_
                            float* partial);
 
 /* ---------------------------------------------------------------------------------------------
+ * The clipped PPO loss of one update minibatch and its gradients (SURVEY §8 A13;
+ * ppo_continuous_action_isaacgym.py:314-349: Normal(mean, exp(logstd)).log_prob(action).sum(1), the
+ * ratio to the rollout's log-prob, the clipped surrogate, the (optionally clipped) value loss, the
+ * entropy, loss = pg_loss - ent_coef entropy_loss + vf_coef v_loss, and old_approx_kl / approx_kl /
+ * clipfrac), in two launches.  Replaces torch's loss expressions and their autograd (~100 kernels).
+ *   mean, action (rows_pad, n_act); value (rows_pad,) the critic output; logstd (n_act,);
+ *   logprob_old, adv, returns, values_old (rows,) the minibatch's stored rows (adv already normalised);
+ *   clip_lo / clip_hi: 1 - clip_coef and 1 + clip_coef as fp32 (the clamp bounds);
+ *   grad_mean (rows_pad, n_act), grad_value (rows_pad,), grad_logstd (n_act,): d loss / d input, with
+ *     torch's conventions at the kinks (maximum splits a tie in half, clamp passes [lo, hi]); rows
+ *     [rows, rows_pad) (padding copies the loss does not see) get zero;
+ *   loss_out[1] = loss; stats_out[6] = pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac;
+ *   partial: scratch of vss_ppo_loss_scratch_floats(rows_pad, n_act) floats (-1 for a bad size),
+ *     reduced in a fixed order (deterministic).
+ * n_act in {1, 2, 3, 4, 6, 8}; every pointer 4-B aligned.
+ * ------------------------------------------------------------------------------------------- */
+int64_t vss_ppo_loss_scratch_floats(int64_t rows_pad, int32_t n_act);
+int vss_ppo_loss(void* stream, int64_t rows, int64_t rows_pad, int32_t n_act, const float* mean, const float* logstd,
+                 const float* value, const float* action, const float* logprob_old, const float* adv,
+                 const float* returns, const float* values_old, float clip_coef, float clip_lo, float clip_hi,
+                 float ent_coef, float vf_coef, int32_t clip_vloss, float* grad_mean, float* grad_value,
+                 float* grad_logstd, float* loss_out, float* stats_out, float* partial);
+
+/* ---------------------------------------------------------------------------------------------
  * Episode statistics: RecordEpisodeStatisticsTorch.step (envs/wrappers.py:66-87)
  * for `rows` learner rows in one launch, in the reference's order:
  *   ep_returns += rews; ep_lengths += 1; returned_returns = ep_returns; returned_lengths =

@@ -1,6 +1,6 @@
 // vss_build_info.cpp — the build's source stamp (include/vss.h vss_source_hash).
-// VSS_SOURCE_HASH is the first 16 hex digits of sha256(vss_step.hip + vss_update.hip +
-// vss_policy.hip + include/vss.h + Makefile), computed by the Makefile at build time; the Python
+// VSS_SOURCE_HASH is the first 16 hex digits of sha256 over the Makefile's STAMPED list (the .hip
+// sources, include/vss.h and the Makefile, in that list's order), computed at build time; the Python
 // loader (vss_amd/_native.py) recomputes it from the tree and refuses a library built from other
 // sources, so a stale prebuilt .so can never be the one that runs.
 #include "../../include/vss.h"

@@ -53,8 +53,10 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+
 enum { EPI_TANH = 0, EPI_DTANH = 1, EPI_TANH_OUT = 2, EPI_WGRAD = 3 };
-enum { ST_ROW = 0, ST_TR = 1, ST_DMA = 2, ST_TR2 = 3 };
+enum { ST_ROW = 0, ST_TR = 1, ST_DMA = 2, ST_TR2 = 3, ST_KROW = 4 };
 
 constexpr int KT = 32;  // K tile = one v_mfma_f32_16x16x32_bf16 step
 // EPI_DTANH: y row groups requested at the item's last K-tile pair (the rest at the epilogue's start);
@@ -105,6 +107,38 @@ struct Img {
   static constexpr int PS = 4 * GS;
   static constexpr int BYTES = 3 * PS;
 };
+
+// ST_KROW image of an R-column operand whose contraction index is its ROW in global memory (the weight
+// gradient's x and grad, (rows, R)): [plane 3][R / 128 sub-tiles][32 contraction rows][128 bf16], i.e.
+// the global layout, 256 B per row, with the 16-B chunks of row r XOR-swizzled by
+// kswz(r) = ((r & 3) << 2) | ((r >> 2) & 3).  The staging writes whole rows (16 B per lane, an 8-lane
+// write group = 8 chunks of one row: conflict-free), and the MFMA fragment -- 8 consecutive contraction
+// rows of one feature -- is read TRANSPOSED with two ds_read_b64_tr_b16 (rows 8 fg + q and 8 fg + 4 + q,
+// MI355X / cdna_hip_programming.md T10): each 32-lane half then touches 16 distinct 16-B slots of the
+// 256-B bank row (layout (b) of T10).  No register transpose and only 16-B global loads: the ST_TR /
+// ST_TR2 staging it replaces gathered each k group of a column with 8 dword loads per lane.
+__device__ __forceinline__ int kswz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+template <int R>
+struct KImg {
+  static constexpr int SUB = 32 * 256;
+  static constexpr int PS = (R / 128) * SUB;
+  static_assert(R % 128 == 0 && 3 * PS == Img<R>::BYTES, "ST_KROW: whole 128-feature sub-tiles, same bytes as Img");
+};
+// byte offset (within one plane of a KImg) of the half-h transposed read of the fragment of features
+// i0 .. i0 + 15 (i0 % 16 == 0): lane 4q + p of 16-lane group fg addresses contraction row 8 fg + 4 h + q,
+// features i0 + 4p .. + 3; lane fr of the group receives feature i0 + fr, rows in elements 0..3
+__device__ __forceinline__ int kfrag_off(int i0, int lane, int h) {
+  const int q = (lane >> 2) & 3, p = lane & 3, row = 8 * (lane >> 4) + 4 * h + q;
+  const int c = ((i0 & 127) >> 3) + (p >> 1);
+  return (i0 >> 7) * (32 * 256) + row * 256 + 16 * (c ^ kswz(row)) + 8 * (p & 1);
+}
+__device__ __forceinline__ u32x4 tr_frag(const char* lds_at_a, const char* lds_at_b) {
+  typedef __attribute__((address_space(3))) i16x4* lp;
+  const i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(lds_at_a));
+  const i16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(lds_at_b));
+  const uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
+  return (u32x4){ua.x, ua.y, ub.x, ub.y};
+}
 
 template <int BI_, int BJ_, int WI_, int WJ_>
 struct Cfg {
@@ -174,7 +208,13 @@ __device__ __forceinline__ void load_op(u32x4 (*dst)[2], const void* base_, int6
 #pragma unroll
   for (int u = 0; u < NP; ++u) {
     const int pr = t + C::THREADS * u;
-    if constexpr (MODE == ST_ROW) {
+    if constexpr (MODE == ST_KROW) {
+      // 8 consecutive features of one contraction row: a wave reads R / 8 lanes x 32 B per row
+      const int row = pr / (R / 8), cc = pr % (R / 8);
+      const float* src = static_cast<const float*>(base_) + (k0 + row) * ld + 8 * cc;
+      dst[u][0] = *reinterpret_cast<const u32x4*>(src);
+      dst[u][1] = *reinterpret_cast<const u32x4*>(src + 4);
+    } else if constexpr (MODE == ST_ROW) {
       const int g = (pr >> 3) & 3, row = (pr & 7) | ((pr >> 5) << 3);
       const float* src = static_cast<const float*>(base_) + (int64_t)row * ld + k0 + 8 * g;
       dst[u][0] = *reinterpret_cast<const u32x4*>(src);
@@ -213,10 +253,19 @@ __device__ __forceinline__ void write_op(const u32x4 (*src)[2], char* img) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(src[u][e >> 2][e & 3]);
     split8(v, hi, mid, lo);
-    char* d = img + g * Img<R>::GS + row * 16;
+    char* d;
+    int ps;
+    if constexpr (MODE == ST_KROW) {
+      const int kr = pr / (R / 8), cc = pr % (R / 8);
+      d = img + (cc >> 4) * KImg<R>::SUB + kr * 256 + 16 * ((cc & 15) ^ kswz(kr));
+      ps = KImg<R>::PS;
+    } else {
+      d = img + g * Img<R>::GS + row * 16;
+      ps = Img<R>::PS;
+    }
     *reinterpret_cast<u32x4*>(d) = hi;
-    *reinterpret_cast<u32x4*>(d + Img<R>::PS) = mid;
-    *reinterpret_cast<u32x4*>(d + 2 * Img<R>::PS) = lo;
+    *reinterpret_cast<u32x4*>(d + ps) = mid;
+    *reinterpret_cast<u32x4*>(d + 2 * ps) = lo;
   }
 }
 
@@ -316,9 +365,10 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     item_ij(w, it, jt, sp);
     fk0 = kt_lo(sp) * KT;
     f_kn = (int)(kt_lo(sp + 1) - kt_lo(sp));
-    if constexpr (SP == ST_TR) fp = static_cast<const char*>(a.p) + (int64_t)it * BI * 4;
+    if constexpr (SP == ST_TR || SP == ST_KROW) fp = static_cast<const char*>(a.p) + (int64_t)it * BI * 4;
     else fp = static_cast<const char*>(a.p);  // ST_DMA: addressed by dma_p
-    if constexpr (SQ == ST_TR || SQ == ST_TR2) fq = reinterpret_cast<const char*>(a.q) + (int64_t)jt * BJ * 4;
+    if constexpr (SQ == ST_TR || SQ == ST_TR2 || SQ == ST_KROW)
+      fq = reinterpret_cast<const char*>(a.q) + (int64_t)jt * BJ * 4;
     else fq = reinterpret_cast<const char*>(a.q) + (int64_t)jt * BJ * a.ldq * 4;
   };
   point(f_item);
@@ -365,12 +415,28 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     const char* pb = lds + buf * C::BUF + fg * Img<BI>::GS + (wi * C::WTI + fr) * 16;
     const char* qb = lds + buf * C::BUF + Img<BI>::BYTES + fg * Img<BJ>::GS + (wj * C::WTJ + fr) * 16;
     u32x4 pf[3][TI], qf[3][TJ];
+    const char* pk = lds + buf * C::BUF;                    // ST_KROW images: plane 0 of P
+    const char* qk = lds + buf * C::BUF + Img<BI>::BYTES;  // and of Q
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) {
 #pragma unroll
-      for (int i = 0; i < TI; ++i) pf[pl][i] = *reinterpret_cast<const u32x4*>(pb + pl * Img<BI>::PS + i * 256);
+      for (int i = 0; i < TI; ++i) {
+        if constexpr (SP == ST_KROW) {
+          const int i0 = wi * C::WTI + 16 * i;
+          pf[pl][i] = tr_frag(pk + pl * KImg<BI>::PS + kfrag_off(i0, lane, 0), pk + pl * KImg<BI>::PS + kfrag_off(i0, lane, 1));
+        } else {
+          pf[pl][i] = *reinterpret_cast<const u32x4*>(pb + pl * Img<BI>::PS + i * 256);
+        }
+      }
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) qf[pl][j] = *reinterpret_cast<const u32x4*>(qb + pl * Img<BJ>::PS + j * 256);
+      for (int j = 0; j < TJ; ++j) {
+        if constexpr (SQ == ST_KROW) {
+          const int j0 = wj * C::WTJ + 16 * j;
+          qf[pl][j] = tr_frag(qk + pl * KImg<BJ>::PS + kfrag_off(j0, lane, 0), qk + pl * KImg<BJ>::PS + kfrag_off(j0, lane, 1));
+        } else {
+          qf[pl][j] = *reinterpret_cast<const u32x4*>(qb + pl * Img<BJ>::PS + j * 256);
+        }
+      }
     }
     if constexpr (PDMA) {
       __builtin_amdgcn_sched_barrier(0);
@@ -716,7 +782,7 @@ int vss_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_
   a.q = grad;
   a.ldo = k_in;
   a.out = partial;
-  return launch<EPI_WGRAD, ST_TR, ST_TR2, CfgA>(stream, a, wg_plan(rows, n_out, k_in));
+  return launch<EPI_WGRAD, ST_KROW, ST_KROW, CfgA>(stream, a, wg_plan(rows, n_out, k_in));
 }
 
 }  // extern "C"

@@ -22,7 +22,8 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "vss.h"
 
 # the sources the Makefile stamps into the library, in its order (csrc/Makefile STAMPED)
 STAMPED = (os.path.join(CSRC, "vss_step.hip"), os.path.join(CSRC, "vss_update.hip"),
-           os.path.join(CSRC, "vss_policy.hip"), os.path.join(CSRC, "vss_gemm_x6.hip"), HEADER,
+           os.path.join(CSRC, "vss_policy.hip"), os.path.join(CSRC, "vss_gemm_x6.hip"),
+           os.path.join(CSRC, "vss_loss.hip"), HEADER,
            os.path.join(CSRC, "Makefile"))
 
 ABI_VERSION = 2
@@ -37,7 +38,7 @@ EXPORTED = ("vss_abi_version", "vss_source_hash", "vss_error_string", "vss_step"
             "vss_linear_tanh", "vss_linear_tanh_out", "vss_linear_tanh_backward_chunks", "vss_linear_tanh_backward",
             "vss_output_backward_chunks", "vss_output_backward", "vss_linear_tanh_bf16x6",
             "vss_linear_tanh_out_bf16x6", "vss_linear_tanh_backward_chunks_bf16x6", "vss_linear_tanh_backward_bf16x6",
-            "vss_weight_grad_chunks_bf16x6", "vss_weight_grad_bf16x6")
+            "vss_weight_grad_chunks_bf16x6", "vss_weight_grad_bf16x6", "vss_ppo_loss_scratch_floats", "vss_ppo_loss")
 
 
 class VssParams(ctypes.Structure):
@@ -91,9 +92,14 @@ def source_hash() -> str:
 
 def verify_source_hash(lib: ctypes.CDLL, expected: str | None = None) -> None:
     """Raise unless the library was built from the tree's sources (a stale prebuilt .so)."""
-    lib.vss_source_hash.restype = ctypes.c_char_p
-    built = lib.vss_source_hash().decode()
     want = source_hash() if expected is None else expected
+    try:
+        fn = lib.vss_source_hash
+    except AttributeError:  # a library older than the stamp: stale by definition
+        fn = None
+    if fn is not None:
+        fn.restype = ctypes.c_char_p
+    built = fn().decode() if fn is not None else "<no vss_source_hash symbol>"
     if built != want:
         raise NativeError(
             f"{LIB_PATH} was built from other sources (stamp {built}, tree {want}); rebuild it with "
@@ -167,6 +173,11 @@ def load() -> ctypes.CDLL:
     L.vss_weight_grad_chunks_bf16x6.restype = i64
     L.vss_weight_grad_bf16x6.argtypes = [P, i64, i32, i32, P, P, P]
     L.vss_weight_grad_bf16x6.restype = ctypes.c_int
+    f32 = ctypes.c_float
+    L.vss_ppo_loss_scratch_floats.argtypes = [i64, i32]
+    L.vss_ppo_loss_scratch_floats.restype = i64
+    L.vss_ppo_loss.argtypes = [P, i64, i64, i32] + [P] * 8 + [f32] * 5 + [i32] + [P] * 6
+    L.vss_ppo_loss.restype = ctypes.c_int
     if L.vss_abi_version() != ABI_VERSION:
         raise NativeError(f"libvss_amd ABI {L.vss_abi_version()} != expected {ABI_VERSION}")
     _lib = L

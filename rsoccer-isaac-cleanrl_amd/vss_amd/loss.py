@@ -1,0 +1,106 @@
+"""The clipped PPO loss of one update minibatch (csrc/vss_loss.hip, include/vss.h vss_ppo_loss):
+
+    loss, stats = ppo_loss(mean, logstd, value, action, logprob_old, adv, returns, values_old,
+                           clip_coef, ent_coef, vf_coef, clip_vloss)
+
+the reference's minibatch loss (ppo_continuous_action_isaacgym.py:318-349) from the networks' outputs:
+`mean` (rows_pad, n_act) the actor's output, `logstd` (1, n_act) the Agent's actor_logstd, `value`
+(rows_pad, 1) the critic's output, and the minibatch's stored rows (the first `rows` = len(logprob_old)
+rows of the network outputs; rows beyond are padding the loss does not see).  `stats` = (pg_loss,
+v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac), 0-dim tensors without gradient.  One autograd
+node: the forward launch also writes d loss / d (mean, logstd, value), which the backward scales by the
+incoming gradient.  On a ROCm device it runs the HIP kernels (and raises if the library is missing);
+CPU tensors take the reference's torch expressions (`reference_loss`)."""
+from __future__ import annotations
+
+import torch
+from torch.distributions.normal import Normal
+
+from . import _native as N
+
+N_ACT = (1, 2, 3, 4, 6, 8)
+
+
+def reference_loss(mean, logstd, value, action, logprob_old, adv, returns, values_old, clip_coef, ent_coef, vf_coef,
+                   clip_vloss):
+    """The reference's expressions (ppo…:318-349; Agent.get_action_and_value ppo…:157-164), torch autograd."""
+    n = logprob_old.shape[0]
+    probs = Normal(mean, torch.exp(logstd.expand_as(mean)), validate_args=False)
+    newlogprob = probs.log_prob(action).sum(1)[:n]
+    entropy = probs.entropy().sum(1)[:n]
+    newvalue = value[:n].view(-1)
+    logratio = newlogprob - logprob_old
+    ratio = logratio.exp()
+    with torch.no_grad():
+        old_approx_kl = (-logratio).mean()
+        approx_kl = ((ratio - 1) - logratio).mean()
+        clipfrac = ((ratio - 1.0).abs() > clip_coef).float().mean()
+    pg_loss = torch.max(-adv * ratio, -adv * torch.clamp(ratio, 1 - clip_coef, 1 + clip_coef)).mean()
+    if clip_vloss:
+        v_unclipped = (newvalue - returns) ** 2
+        v_clipped = values_old + torch.clamp(newvalue - values_old, -clip_coef, clip_coef)
+        v_loss = 0.5 * torch.max(v_unclipped, (v_clipped - returns) ** 2).mean()
+    else:
+        v_loss = 0.5 * ((newvalue - returns) ** 2).mean()
+    entropy_loss = entropy.mean()
+    loss = pg_loss - ent_coef * entropy_loss + v_loss * vf_coef
+    return loss, (pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac)
+
+
+def ppo_loss_ok(mean: torch.Tensor, value: torch.Tensor) -> bool:
+    """Inputs the HIP loss takes: fp32 ROCm tensors, n_act in N_ACT, value one column."""
+    return mean.is_cuda and mean.dtype == torch.float32 and value.dtype == torch.float32 and mean.dim() == 2 \
+        and mean.shape[1] in N_ACT and value.numel() == mean.shape[0]
+
+
+class _PPOLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mean, logstd, value, action, logprob_old, adv, returns, values_old, clip_coef, ent_coef, vf_coef,
+                clip_vloss):
+        rows, rows_pad, n_act = logprob_old.shape[0], mean.shape[0], mean.shape[1]
+        lib = N.load()
+        dev = mean.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        mean, value, action = mean.contiguous(), value.contiguous(), action.contiguous()
+        logstd_c = logstd.reshape(-1).contiguous()
+        ins = [t.contiguous() for t in (logprob_old, adv, returns, values_old)]
+        g_mean = torch.empty((rows_pad, n_act), **f32)
+        g_value = torch.empty((rows_pad, 1), **f32)
+        g_logstd = torch.empty((1, n_act), **f32)
+        loss = torch.empty((), **f32)
+        stats = torch.empty(6, **f32)
+        part = torch.empty(lib.vss_ppo_loss_scratch_floats(rows_pad, n_act), **f32)
+        c = float(clip_coef)  # ctypes rounds the clamp bounds to fp32 as torch.clamp does
+        N.check(lib.vss_ppo_loss(N.stream_of(dev), rows, rows_pad, n_act, mean.data_ptr(), logstd_c.data_ptr(),
+                                 value.data_ptr(), action.data_ptr(), *[t.data_ptr() for t in ins], c, 1 - c, 1 + c,
+                                 float(ent_coef), float(vf_coef), int(bool(clip_vloss)), g_mean.data_ptr(),
+                                 g_value.data_ptr(), g_logstd.data_ptr(), loss.data_ptr(), stats.data_ptr(),
+                                 part.data_ptr()),
+                "vss_ppo_loss")
+        ctx.save_for_backward(g_mean, g_logstd, g_value)
+        ctx.mark_non_differentiable(stats)
+        return loss, stats
+
+    @staticmethod
+    def backward(ctx, g_loss, _g_stats):
+        g_mean, g_logstd, g_value = ctx.saved_tensors
+        return (g_mean * g_loss, g_logstd * g_loss, g_value * g_loss) + (None,) * 9
+
+
+def ppo_loss(mean, logstd, value, action, logprob_old, adv, returns, values_old, clip_coef, ent_coef, vf_coef,
+             clip_vloss):
+    rows = logprob_old.shape[0]
+    if mean.dim() != 2 or action.shape[1:] != mean.shape[1:] or action.shape[0] < rows or mean.shape[0] < rows \
+            or value.shape[0] != mean.shape[0] or logstd.numel() != mean.shape[1] \
+            or not (adv.shape == returns.shape == values_old.shape == logprob_old.shape):
+        raise ValueError(f"ppo_loss: mean {tuple(mean.shape)}, value {tuple(value.shape)}, action {tuple(action.shape)}, "
+                         f"logstd {tuple(logstd.shape)}, minibatch rows {tuple(logprob_old.shape)}")
+    if not mean.is_cuda:
+        return reference_loss(mean, logstd, value, action[:mean.shape[0]], logprob_old, adv, returns, values_old,
+                              clip_coef, ent_coef, vf_coef, clip_vloss)
+    if not ppo_loss_ok(mean, value) or rows == 0:
+        raise ValueError(f"vss_ppo_loss: fp32 ROCm tensors with n_act in {N_ACT} and rows > 0 required, "
+                         f"got {mean.dtype} {tuple(mean.shape)}")
+    loss, stats = _PPOLoss.apply(mean, logstd, value.reshape(-1, 1), action[:mean.shape[0]], logprob_old, adv, returns,
+                                 values_old, clip_coef, ent_coef, vf_coef, clip_vloss)
+    return loss, tuple(stats[i] for i in range(6))

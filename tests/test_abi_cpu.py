@@ -40,6 +40,16 @@ def test_library_is_built_from_the_tree_sources():
         N.verify_source_hash(lib, expected="0" * 16)
 
 
+def test_library_without_stamp_symbol_is_refused():
+    """A library older than the stamp (no vss_source_hash symbol) raises NativeError with the rebuild
+    hint, not an AttributeError."""
+    class NoStamp:  # ctypes.CDLL raises AttributeError for a symbol the library does not export
+        def __getattr__(self, name):
+            raise AttributeError(name)
+    with pytest.raises(N.NativeError, match="make -C"):
+        N.verify_source_hash(NoStamp())
+
+
 def test_stale_library_is_refused_at_load(tmp_path, monkeypatch):
     """load() itself refuses a library whose stamp does not match the tree (here: the tree's
     stamped sources replaced by a modified copy of one of them)."""

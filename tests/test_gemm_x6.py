@@ -90,6 +90,47 @@ def test_x6_weight_grad_error_at_most_fp32_gpu(rows, n_out, k_in):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [128, 384])
+def test_x6_persistent_multi_item_cfga_gpu(n):
+    """Widths that are not multiples of 256 take the 128-feature x 256-row block (CfgA); at 131,072 rows
+    every block runs several work items (n = 128: 512 items on 256 blocks; n = 384: 1,536 items on
+    240 blocks with a fixed i tile per block), so the bias and column-sum bookkeeping of one i tile
+    per block is exercised across items.  Forward, backward and the column sums vs fp64."""
+    rows, k = 131072, 256
+    x, w, b, _, _ = _ops(rows, k, n, n)
+    ref = torch.tanh(x.double() @ w.double().t() + b.double())
+    e6 = _rel(linear_tanh_x6(x, w, b), ref)
+    assert e6[0] < 4e-6, e6
+    # backward from this n-wide layer into a k-wide tanh layer: P = W^T (k, n) -> n_out = k = 256 (CfgB)
+    # and from a k-wide layer into the n-wide one: n_out = n (CfgA, multi-item)
+    g = torch.Generator(device="cuda").manual_seed(n + 1)
+    w2 = torch.randn(k, n, device="cuda", generator=g) / k ** 0.5
+    g_next = torch.randn(rows, k, device="cuda", generator=g) * 1e-3
+    y_n = torch.tanh(torch.randn(rows, n, device="cuda", generator=g))
+    refb = (g_next.double() @ w2.double()) * (1 - y_n.double() ** 2)
+    gz, db = linear_tanh_backward_x6(g_next, w2, y_n)
+    eb = _rel(gz, refb)
+    et = _rel(g_next.mm(w2) * (1 - y_n * y_n), refb)
+    assert eb[0] < 4e-6 and eb[1] < 1.25 * et[1] + 1e-8, (eb, et)
+    torch.testing.assert_close(db.double(), refb.sum(0), rtol=1e-5, atol=1e-5 * float(refb.sum(0).abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_out,k_in", [(256, 384), (512, 384)])
+def test_x6_weight_grad_k_in_384_gpu(n_out, k_in):
+    """k_in = 384 (3 i tiles): the grid trim (grid -= grid % 8) leaves some blocks two work items;
+    the result against fp64 at the fp32 GEMM's error."""
+    rows = 65536 + 64
+    g = torch.Generator(device="cuda").manual_seed(n_out + k_in)
+    gz = torch.randn(rows, n_out, device="cuda", generator=g) * 1e-3
+    x = torch.tanh(torch.randn(rows, k_in, device="cuda", generator=g))
+    ref = gz.double().t() @ x.double()
+    e6 = _rel(weight_grad_x6(gz, x), ref)
+    et = _rel(gz.t().mm(x), ref)
+    assert e6[0] < 4e-6 and e6[1] < 1.25 * et[1] + 1e-8, (e6, et)
+
+
+@pytest.mark.gpu
 def test_x6_exact_on_integer_operands_gpu():
     """Integer operands with exact fp32 sums: every entry point returns the exact result (the split of
     an integer of <= 24 bits is exact, the six products carry all of it for <= 16-bit factors)."""

@@ -525,6 +525,9 @@ def value_loss(newvalue, mb_returns, mb_values, clip_coef: float, clip_vloss: bo
 # hidden-layer GEMM runs on whole x6 tiles: at 4,095 envs a 131,040-row minibatch otherwise leaves
 # 224-row tails that hipBLASLt runs on one or two workgroups (43-110 us each, ~21 ms per update)
 MLP_ROW_PAD = 256
+# MinibatchGraph re-runs this replay eagerly and compares the two bit for bit (once per training run;
+# round 3's packet-capture failure began at the 9th replay, profiles/r03w_graph_probe2.log)
+GRAPH_CHECK_REPLAY = 12
 
 
 def minibatch_losses(agent, args, obs, actions, logprobs, adv, returns, values):
@@ -566,6 +569,8 @@ class MinibatchGraph:
         self.graph = None
         self.warm = False
         self.out = None
+        self.replays = 0
+        self.failed = False  # a self-check found the replay differing from eager: eager from then on
 
     def _body(self):
         self.flat.zero()
@@ -602,13 +607,35 @@ class MinibatchGraph:
         torch.index_select(b_returns, 0, inds, out=self.ret)
         torch.index_select(b_values, 0, inds, out=self.val)
         self.adv.copy_(mb_adv)
+        if self.failed:
+            return self._body()
         if self.graph is None:
             if not self.warm:  # the first minibatch: eager, real work
                 self.warm = True
                 return self._body()
             self._capture()
         self.graph.replay()
+        self.replays += 1
+        if self.replays == GRAPH_CHECK_REPLAY:
+            return self._check()
         return self.out
+
+    def _check(self):
+        """Self-check of one replay: the same minibatch again, eagerly, on the same static inputs; the
+        replay's statistics and gradients must equal the eager ones bit for bit (the kernels and their
+        order are the same).  On a difference the graph is dropped and every later minibatch runs
+        eagerly (the eager result, already in FlatGrads, is this minibatch's)."""
+        got = [t.clone() for t in self.out] + [self.flat.flat.clone()]
+        want = list(self._body())
+        same = all(torch.equal(a, b) for a, b in zip(got, want + [self.flat.flat]))
+        if same:
+            return self.out
+        import warnings
+        warnings.warn(f"MinibatchGraph: replay {self.replays} differs from the eager minibatch; the update runs "
+                      f"eagerly from here on (DEBUG_CLR_GRAPH_PACKET_CAPTURE="
+                      f"{os.environ.get(_PACKET_CAPTURE, '<unset>')})", RuntimeWarning)
+        self.failed, self.graph = True, None
+        return tuple(want)
 
 
 def padding_rows(mb: int, device) -> int:

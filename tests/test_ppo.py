@@ -201,6 +201,51 @@ def test_minibatch_graph_update_equals_eager_gpu(n, nmb, epochs, updates, norm_a
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_minibatch_graph_self_check_gpu(corrupt):
+    """MinibatchGraph re-runs replay GRAPH_CHECK_REPLAY eagerly and compares the two bit for bit.  A
+    healthy graph passes and stays in use; a replay whose gradients are corrupted (here: injected into
+    FlatGrads after that replay) is caught, the minibatch takes the eager result, the graph is dropped
+    and the rest of the update runs eagerly -- the update then equals the eager one exactly."""
+    args = _args(norm_adv=True, clip_vloss=False, num_minibatches=4, update_epochs=4)  # 16 minibatches
+    n = 32768
+    obs, act, logp, adv, ret, val = [t.cuda() for t in _synthetic_batch(5, n)]
+    res = []
+    for use_graph in (False, True):
+        agent = make_agent(2).cuda()
+        flat = P.FlatGrads(agent)
+        opt = torch.optim.Adam(agent.parameters(), lr=1e-3, eps=1e-5)
+        graph = P.make_minibatch_graph(agent, flat, args, n, (52,), (2,), "cuda") if use_graph else None
+        if graph is not None and corrupt:
+            capture = graph._capture
+
+            class Corrupting:  # the captured graph, with a wrong gradient after the checked replay
+                def __init__(self, g):
+                    self.g = g
+
+                def replay(self):
+                    self.g.replay()
+                    if graph.replays + 1 == P.GRAPH_CHECK_REPLAY:
+                        flat.flat[7] += 1.0
+
+            def capture_and_corrupt():
+                capture()
+                graph.graph = Corrupting(graph.graph)
+            graph._capture = capture_and_corrupt
+        gen = torch.Generator(device="cuda").manual_seed(7)
+        if use_graph and corrupt:
+            with pytest.warns(RuntimeWarning, match="differs from the eager minibatch"):
+                P.ppo_update(agent, opt, flat, args, obs, logp, act, adv, ret, val, gen=gen, graph=graph)
+        else:
+            P.ppo_update(agent, opt, flat, args, obs, logp, act, adv, ret, val, gen=gen, graph=graph)
+        res.append(torch.cat([p.detach().reshape(-1) for p in agent.parameters()]))
+        if graph is not None:
+            assert graph.replays >= P.GRAPH_CHECK_REPLAY
+            assert graph.failed == corrupt and (graph.graph is None) == corrupt
+    assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [2000, 262080])
 def test_padded_minibatch_update_matches_unpadded_gpu(n, monkeypatch):
     """The update's minibatch rows padded to whole 256-row GEMM tiles (MLP_ROW_PAD; the padding rows
@@ -279,6 +324,26 @@ def test_train_sa_65536_envs_config3(tmp_path):
     for k in ("v_loss", "pg_loss", "entropy", "approx_kl", "old_approx_kl", "clipfrac", "mean_return"):
         assert np.isfinite(h[k]), (k, h)
     assert h["rollout_s"] > 0 and h["update_s"] > 0 and h["sps"] > 0 and h["episodes"] > 0
+    assert abs(h["entropy"] - 2 * (0.5 + 0.5 * np.log(2 * np.pi))) < 0.1  # logstd starts at 0
+    assert 0 <= h["clipfrac"] <= 1 and h["approx_kl"] < 0.1
+
+
+@pytest.mark.gpu
+def test_train_dma_65536_fields_config4(tmp_path):
+    """BASELINE config 4: PPO-DMA (every blue robot its own agent row, envs/wrappers.py:150-180) at
+    65,536 fields = 196,608 agent rows with the reference's update defaults, one update (6.3 M-row
+    minibatches): num_envs = 3 x fields, every agent-step counted, finite losses, the entropy near its
+    initial value, and the DMA contract's per-robot episodes recorded."""
+    args = P.parse_args(["--env-id", "dma", "--num-envs", str(3 * 65536), "--num-updates", "1",
+                         "--save-path", str(tmp_path), "--log", "false"])
+    assert (args.num_steps, args.update_epochs, args.num_minibatches) == (128, 8, 4)
+    assert args.minibatch_size == 3 * 65536 * 128 // 4
+    agent, hist = P.train(args)
+    (h,) = hist
+    assert h["global_step"] == 3 * 65536 * 128
+    for k in ("v_loss", "pg_loss", "entropy", "approx_kl", "old_approx_kl", "clipfrac", "mean_return"):
+        assert np.isfinite(h[k]), (k, h)
+    assert h["rollout_s"] > 0 and h["update_s"] > 0 and h["episodes"] > 0
     assert abs(h["entropy"] - 2 * (0.5 + 0.5 * np.log(2 * np.pi))) < 0.1  # logstd starts at 0
     assert 0 <= h["clipfrac"] <= 1 and h["approx_kl"] < 0.1
 

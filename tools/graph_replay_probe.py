@@ -12,9 +12,12 @@ Stages (STAGES, comma separated), each captured and replayed REPLAYS times:
   mlp       the actor MLP's forward + backward (_TanhMLP, or torch's nn.Sequential for PATH=torch)
   minibatch MinibatchGraph's body (forward, losses, backward into FlatGrads)
 
-PATH selects the update's MLP arithmetic: x6 (default product), fp32 (VSS_UPDATE_GEMM=fp32), split
-(VSS_UPDATE_MLP=split: hipBLASLt + vss_tanh_grad_bias), torch (plain nn.Sequential: no kernel of
-this repository in the graph).  Set DEBUG_CLR_GRAPH_PACKET_CAPTURE on the command line."""
+PATH_MLP selects the update's MLP arithmetic: x6 (default product), fp32 (VSS_UPDATE_GEMM=fp32), split
+(VSS_UPDATE_MLP=split: hipBLASLt + vss_tanh_grad_bias), torch (plain nn.Sequential); LOSS selects the
+minibatch loss: fused (vss_ppo_loss, default) or torch (the reference's expressions).  PATH_MLP=torch
+LOSS=torch puts no kernel of this repository in the graph.  Set DEBUG_CLR_GRAPH_PACKET_CAPTURE on the
+command line.  NOISE > 0 launches that many tiny eager kernels after each replay; stage ppo runs the
+original failure's setting (ppo_update, 8 epochs x 2 minibatches, captured vs eager)."""
 import os
 import sys
 
@@ -34,6 +37,12 @@ from vss_amd import update as U  # noqa: E402
 
 if PATH == "torch":
     P._mlp_forward = lambda seq, x: seq(x)
+# LOSS=torch: the minibatch loss as the reference's torch expressions and their autograd (~100 small
+# kernels; what the update ran before vss_ppo_loss) instead of the fused HIP loss
+LOSS = os.environ.get("LOSS", "fused")
+if LOSS == "torch":
+    from vss_amd.loss import reference_loss
+    P.ppo_loss = reference_loss
 
 R = int(os.environ.get("REPLAYS", 16))
 MB = int(os.environ.get("MB", 2097152))
@@ -169,7 +178,7 @@ def stage_ppo():
 
 def main():
     print(f"DEBUG_CLR_GRAPH_PACKET_CAPTURE={os.environ.get('DEBUG_CLR_GRAPH_PACKET_CAPTURE', '<unset>')} "
-          f"PATH_MLP={PATH} MB={MB} REPLAYS={R} NOISE={NOISE} torch {torch.__version__} hip {torch.version.hip}", flush=True)
+          f"PATH_MLP={PATH} LOSS={LOSS} MB={MB} REPLAYS={R} NOISE={NOISE} torch {torch.__version__} hip {torch.version.hip}", flush=True)
     ok = True
     for st in os.environ.get("STAGES", "kernel,mlp,minibatch").split(","):
         ok &= {"kernel": stage_kernel, "mlp": stage_mlp, "minibatch": stage_minibatch, "ppo": stage_ppo}[st]()

@@ -35,8 +35,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "rsoccer-isaac-cleanrl_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 
-# before torch initialises the GPU: the PPO leg's captured minibatch needs ROCm's graph packet capture
-# off (ppo_continuous_action_isaacgym.py UPDATE_GRAPH_SAFE)
+# before torch initialises the GPU: the PPO legs run with ROCm's graph packet capture off
+# (ppo_continuous_action_isaacgym.py disable_graph_packet_capture; the captured minibatch also checks itself)
 os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -327,8 +327,9 @@ def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
                                   "products, fp32 accumulation; csrc/vss_gemm_x6.hip)",
                             "fp32": "fp32 MFMA (csrc/vss_update.hip)"}.get(P.UPDATE_GEMM, P.UPDATE_GEMM),
             "update_minibatch": ("one captured HIP graph per minibatch (forward, losses, backward), "
-                                 f"rows padded to {P.MLP_ROW_PAD}" if P.UPDATE_GRAPH_SAFE and args.update_graph
-                                 else "eager"),
+                                 f"rows padded to {P.MLP_ROW_PAD}, replay {P.GRAPH_CHECK_REPLAY} checked against eager"
+                                 if args.update_graph else "eager"),
+            "graph_packet_capture_env": os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "<unset>"),
             "gradient_exchange": ("one flat fp32 all-reduce per minibatch "
                                   f"({dist.get_backend() if dist.is_initialized() else 'none'})") if world > 1 else "none",
             "updates_run": len(hist), "env_steps_run": hist[-1]["global_step"],

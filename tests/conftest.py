@@ -3,8 +3,8 @@ import sys
 
 import pytest
 
-# before any test initialises the GPU: the update's captured minibatch needs ROCm's graph packet
-# capture off (ppo_continuous_action_isaacgym.py UPDATE_GRAPH_SAFE)
+# before any test initialises the GPU: ROCm's graph packet capture off, as the entry points start it
+# (ppo_continuous_action_isaacgym.py disable_graph_packet_capture)
 os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -486,3 +486,16 @@ def test_post_training_evaluation_gpu(tmp_path):
         assert {"Validation/Score/zero", "Validation/Score/ou", "Validation/Score Mean", "Validation/Length Mean"} <= set(res)
         assert all(-1.0 <= res[k] <= 1.0 for k in res if "Score" in k)
         assert res["Validation/Length Mean"] > 0
+
+
+def test_importing_the_train_module_changes_no_environment_variable():
+    """The training module is importable as a library without side effects on the process environment
+    (the packet-capture switch is set only by the entry points: disable_graph_packet_capture)."""
+    import subprocess
+    import sys
+    code = ("import os, sys; sys.path.insert(0, {pkg!r}); env = dict(os.environ); "
+            "os.environ.pop('DEBUG_CLR_GRAPH_PACKET_CAPTURE', None); env.pop('DEBUG_CLR_GRAPH_PACKET_CAPTURE', None); "
+            "import ppo_continuous_action_isaacgym as P; assert dict(os.environ) == env, 'environment changed'; "
+            "assert P.disable_graph_packet_capture() and os.environ['DEBUG_CLR_GRAPH_PACKET_CAPTURE'] == '0'")
+    pkg = os.path.dirname(P.__file__)
+    subprocess.run([sys.executable, "-c", code.format(pkg=pkg)], check=True, timeout=300)

@@ -46,6 +46,7 @@ class LiveTeam:
 
 
 def main():
+    P.disable_graph_packet_capture()  # an entry point: before anything initialises the GPU
     ap = argparse.ArgumentParser()
     ap.add_argument("--env-id", default="sa", choices=["sa", "cma", "dma"])
     ap.add_argument("--num-envs", type=int, default=4095)

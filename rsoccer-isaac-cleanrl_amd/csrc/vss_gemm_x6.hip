@@ -56,7 +56,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 
 enum { EPI_TANH = 0, EPI_DTANH = 1, EPI_TANH_OUT = 2, EPI_WGRAD = 3 };
-enum { ST_ROW = 0, ST_TR = 1, ST_DMA = 2, ST_TR2 = 3, ST_KROW = 4, ST_PLANE = 5 };
+enum { ST_ROW = 0, ST_TR = 1, ST_DMA = 2, ST_TR2 = 3, ST_KROW = 4 };
 
 constexpr int KT = 32;  // K tile = one v_mfma_f32_16x16x32_bf16 step
 // EPI_DTANH: y row groups requested at the item's last K-tile pair (the rest at the epilogue's start);
@@ -140,16 +140,15 @@ __device__ __forceinline__ u32x4 tr_frag(const char* lds_at_a, const char* lds_a
   return (u32x4){ua.x, ua.y, ub.x, ub.y};
 }
 
-template <int BI_, int BJ_, int WI_, int WJ_, bool SB_ = false>
+template <int BI_, int BJ_, int WI_, int WJ_>
 struct Cfg {
   static constexpr int BI = BI_, BJ = BJ_, WI = WI_, WJ = WJ_;
-  static constexpr bool SB = SB_;  // one LDS buffer (two barriers per K tile) instead of two
   static constexpr int THREADS = 64 * WI * WJ;
   static constexpr int WTI = BI / WI, WTJ = BJ / WJ;  // one wave's output extent
   static constexpr int TI = WTI / 16, TJ = WTJ / 16;  // MFMA tiles per wave
   static constexpr int PI = BI * 4 / THREADS, PJ = BJ * 4 / THREADS;  // (row, group) pairs per thread
   static constexpr int BUF = Img<BI>::BYTES + Img<BJ>::BYTES;
-  static constexpr int LDS = (SB ? 1 : 2) * BUF;
+  static constexpr int LDS = 2 * BUF;
   static_assert(PI * THREADS == BI * 4 && PJ * THREADS == BJ * 4, "staging pairs must tile the block");
   static_assert(WTI == 64, "a wave's i extent is one 64-feature slice (EPI_TANH_OUT)");
   static constexpr int BPC = 2 * LDS <= 160 * 1024 ? 2 : 1;  // blocks per CU (LDS-limited)
@@ -162,13 +161,6 @@ using CfgA = Cfg<128, 256, 2, 4>;
 // large, still arrives by LDS-DMA: forward 8-10 %, backward 1-2 % faster, the same bits
 // (profiles/r03z_gemm_x6_fb256.log)
 using CfgB = Cfg<256, 128, 4, 2>;
-// split phase: 128 x 128 blocks of 4 waves on ONE LDS buffer (48 KB), two blocks per CU, so each SIMD
-// runs one wave of each block; the blocks of the grid's second half start half a work item late, so
-// the two blocks of a CU stay out of phase and one block's epilogue (stores, y loads, VALU) overlaps
-// the other block's K loop (MFMAs) instead of every wave of the CU reaching its epilogue together.
-// The weight planes are register-staged from the pre-split image (ST_PLANE): no LDS-DMA, whose
-// completion hipcc waits for by draining every load at the barrier.
-using CfgS = Cfg<128, 128, 2, 2, true>;
 
 struct Args {
   int32_t ni, nj;          // i tiles, j tiles (of BI, BJ)
@@ -187,7 +179,6 @@ struct Args {
   float* partial;          // EPI_DTANH: (grid / ni, I) column sums of out
   const float* w_out;      // EPI_TANH_OUT: (KO, I)
   float* out_part;         // EPI_TANH_OUT: (I / 64, J, KO)
-  int32_t delay;           // CfgS: s_sleep(127) rounds before the grid's second half starts
 };
 
 // one thread's register-staged operands of one K tile: NP groups of 8 raw fp32 values
@@ -199,17 +190,6 @@ struct Stage {
 template <int MODE, int R, int NP, class C>
 __device__ __forceinline__ void load_op(u32x4 (*dst)[2], const void* base_, int64_t ld, int64_t k0) {
   const int t = threadIdx.x;
-  if constexpr (MODE == ST_PLANE) {
-    // the pre-split weight image of K tile k0 / KT (split_image_kernel: exactly the LDS image's bytes),
-    // 16 B per lane, lane-contiguous
-    static_assert(NP * 2 * C::THREADS * 16 == Img<R>::BYTES, "ST_PLANE: whole 16-B chunks per thread");
-    const char* src = static_cast<const char*>(base_) + (k0 / KT) * Img<R>::BYTES;
-#pragma unroll
-    for (int u = 0; u < NP; ++u)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) dst[u][h] = *reinterpret_cast<const u32x4*>(src + (t + C::THREADS * (2 * u + h)) * 16);
-    return;
-  }
   if constexpr (MODE == ST_TR2) {
     // ST_TR with two adjacent columns (image rows) per lane: one 8-B load per contraction row, half
     // the load instructions for the same bytes (a wave reads 512 contiguous bytes of a row); weight
@@ -251,13 +231,6 @@ __device__ __forceinline__ void load_op(u32x4 (*dst)[2], const void* base_, int6
 template <int MODE, int R, int NP, class C>
 __device__ __forceinline__ void write_op(const u32x4 (*src)[2], char* img) {
   const int t = threadIdx.x;
-  if constexpr (MODE == ST_PLANE) {  // already split: a straight copy
-#pragma unroll
-    for (int u = 0; u < NP; ++u)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) *reinterpret_cast<u32x4*>(img + (t + C::THREADS * (2 * u + h)) * 16) = src[u][h];
-    return;
-  }
 #pragma unroll
   for (int u = 0; u < NP; ++u) {
     const int pr = t + C::THREADS * u;
@@ -343,7 +316,7 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
   // ST_DMA: the weight operand's image is copied global -> LDS by the waves' global_load_lds (3 KB per
   // wave per K tile), only the activations go through registers
   constexpr bool PDMA = SP == ST_DMA;
-  constexpr int PI = PDMA ? 0 : (SP == ST_PLANE ? Img<BI>::BYTES / (32 * C::THREADS) : C::PI);
+  constexpr int PI = PDMA ? 0 : C::PI;
   constexpr int NQ = Img<BI>::BYTES / (C::THREADS / 64) / 1024;  // 1-KB DMA slices per wave per K tile
   static_assert(!PDMA || NQ * (C::THREADS / 64) * 1024 == Img<BI>::BYTES, "DMA slices: whole KB per wave");
   // EPI_DTANH: (WJ, BI) column sums, accumulated item by item
@@ -393,7 +366,6 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     fk0 = kt_lo(sp) * KT;
     f_kn = (int)(kt_lo(sp + 1) - kt_lo(sp));
     if constexpr (SP == ST_TR || SP == ST_KROW) fp = static_cast<const char*>(a.p) + (int64_t)it * BI * 4;
-    else if constexpr (SP == ST_PLANE) fp = static_cast<const char*>(a.p) + (int64_t)it * (2 * a.kpairs) * Img<BI>::BYTES;
     else fp = static_cast<const char*>(a.p);  // ST_DMA: addressed by dma_p
     if constexpr (SQ == ST_TR || SQ == ST_TR2 || SQ == ST_KROW)
       fq = reinterpret_cast<const char*>(a.q) + (int64_t)jt * BJ * 4;
@@ -466,7 +438,7 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
         }
       }
     }
-    if constexpr (PDMA || C::SB) {
+    if constexpr (PDMA) {
       __builtin_amdgcn_sched_barrier(0);
       between();
       __builtin_amdgcn_sched_barrier(0);
@@ -485,20 +457,11 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
   };
 
   Stage<PI + PJ> r0, r1;
-  if constexpr (C::SB) {
-    // the grid's second half starts half a work item late (co-resident blocks out of phase)
-    if (blockIdx.x >= (unsigned)G / 2)
-      for (int d = 0; d < a.delay; ++d) __builtin_amdgcn_s_sleep(127);
-    gload(r0);  // K tile 0
-    swrite(r0, 0);
-    gload(r0);  // K tile 1
-  } else {
-    gload(r0);  // K tile 0
-    dma_p(0, 0);
-    swrite(r0, 0);
-    gload(r1);  // K tile 1
-    gload(r0);  // K tile 2
-  }
+  gload(r0);  // K tile 0
+  dma_p(0, 0);
+  swrite(r0, 0);
+  gload(r1);  // K tile 1
+  gload(r0);  // K tile 2
   __syncthreads();
   int w = slot;
   for (;;) {
@@ -517,28 +480,7 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     f32x4 ypre[EPI == EPI_DTANH ? kYPre : 1][EPI == EPI_DTANH ? TI : 1];
     const int64_t jy = (int64_t)jt * BJ + wj * C::WTJ + fr;
     const int kn = (int)(kt_lo(sp + 1) - kt_lo(sp));  // this item's K tiles (even)
-    for (int kt = 0; C::SB && kt < kn; ++kt) {
-      // one buffer: the K tile's fragments into registers, a barrier, the next K tile (staged one
-      // iteration ago) into the same buffer and the one after it into registers, then the MFMAs from
-      // registers, and a barrier before the next reads
-      if constexpr (EPI == EPI_DTANH) {
-        if (kt + 2 == kn) {
-#pragma unroll
-          for (int j = 0; j < kYPre; ++j)
-#pragma unroll
-            for (int i = 0; i < TI; ++i)
-              ypre[j][i] = *reinterpret_cast<const f32x4*>(a.y + (jy + 16 * j) * a.ldo + it * BI + wi * C::WTI + 16 * i +
-                                                           4 * fg);
-        }
-      }
-      mfma_tile(0, [&] {
-        __syncthreads();
-        swrite(r0, 0);
-        gload(r0);
-      });
-      __syncthreads();
-    }
-    for (int kt = 0; !C::SB && kt < kn; kt += 2) {
+    for (int kt = 0; kt < kn; kt += 2) {
       if constexpr (EPI == EPI_DTANH) {
         if (kt + 2 >= kn) {
 #pragma unroll
@@ -724,9 +666,6 @@ static int launch(void* stream, Args a, const Plan& pl) {
   a.kpairs = pl.kpairs;
   a.items = pl.items;
   a.splits = pl.splits;
-  // CfgS: half a work item of MFMA time (128 x 128 x K x 6 MACs at half a CU's 2,048 MAC/clk), in
-  // s_sleep(127) rounds of 8,128 cycles
-  a.delay = C::SB ? (int32_t)((128 * 128 * 6 * 2 * KT * pl.kpairs / 1024 / 2 + 8127) / 8128) : 0;
   hipLaunchKernelGGL((gemm_x6_kernel<EPI, SP, SQ, C, KO>), dim3((unsigned)pl.grid), dim3(C::THREADS), 0,
                      (hipStream_t)stream, a);
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
@@ -772,7 +711,7 @@ int vss_linear_tanh_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_o
     if (rc != VSS_OK) return rc;
     Args a = fb_args(k_in, n_out, w_split, x, y);
     a.bias = bias;
-    return launch<EPI_TANH, C::SB ? ST_PLANE : ST_DMA, ST_ROW, C>(stream, a, fb_plan<C>(rows, k_in, n_out));
+    return launch<EPI_TANH, ST_DMA, ST_ROW, C>(stream, a, fb_plan<C>(rows, k_in, n_out));
   });
 }
 
@@ -792,10 +731,9 @@ int vss_linear_tanh_out_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t
     a.w_out = w_out;
     a.out_part = out_part;
     const Plan pl = fb_plan<C>(rows, k_in, n_out);
-    constexpr int SP = C::SB ? ST_PLANE : ST_DMA;
-    if (k_out == 1) return launch<EPI_TANH_OUT, SP, ST_ROW, C, 1>(stream, a, pl);
-    if (k_out == 2) return launch<EPI_TANH_OUT, SP, ST_ROW, C, 2>(stream, a, pl);
-    return launch<EPI_TANH_OUT, SP, ST_ROW, C, 6>(stream, a, pl);
+    if (k_out == 1) return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, C, 1>(stream, a, pl);
+    if (k_out == 2) return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, C, 2>(stream, a, pl);
+    return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, C, 6>(stream, a, pl);
   });
 }
 
@@ -823,7 +761,7 @@ int vss_linear_tanh_backward_bf16x6(void* stream, int64_t rows, int32_t k_next, 
     Args a = fb_args(k_next, n_out, w_split, grad_next, grad_in);
     a.y = y;
     a.partial = bias_partial;
-    return launch<EPI_DTANH, C::SB ? ST_PLANE : ST_DMA, ST_ROW, C>(stream, a, fb_plan<C>(rows, k_next, n_out));
+    return launch<EPI_DTANH, ST_DMA, ST_ROW, C>(stream, a, fb_plan<C>(rows, k_next, n_out));
   });
 }
 

@@ -380,6 +380,14 @@ class FlatGrads:
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
             self.flat.mul_(1.0 / world)
 
+    def clip_norm_(self, max_norm: float) -> torch.Tensor:
+        """nn.utils.clip_grad_norm_(agent.parameters(), max_norm) (ppo…:353) on the flat buffer: the L2
+        norm of all the gradients (one reduction instead of one per tensor and a norm of the norms), the
+        same coefficient max_norm / (norm + 1e-6) clamped to 1, one in-place scale.  Returns the norm."""
+        total = torch.linalg.vector_norm(self.flat)
+        self.flat.mul_(torch.clamp(max_norm / (total + 1e-6), max=1.0))
+        return total
+
 
 class _NullWriter:
     def add_scalar(self, *a, **k):
@@ -696,7 +704,7 @@ def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_adv
             pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac = st
             clipfracs.append(clipfrac.clone())  # (a graph's outputs are rewritten by the next replay)
             flat.all_reduce_mean(world)  # the data-parallel exchange (RCCL on ROCm)
-            nn.utils.clip_grad_norm_(agent.parameters(), args.max_grad_norm)
+            flat.clip_norm_(args.max_grad_norm)
             optimizer.step()
 
             if args.adaptative_lr or args.target_kl is not None:
@@ -804,7 +812,9 @@ def train(args, on_update=None):
     if args.fused_policy and device.type == "cuda" and args.amp == "none":
         from vss_amd.policy import FusedPolicy
         fused = FusedPolicy(agent, seed=seed * 7919 + 17)
-    optimizer = optim.Adam(agent.parameters(), lr=args.learning_rate, eps=1e-5)
+    # torch's Adam (ppo…:166) -- on the GPU its fused implementation: one kernel per step instead of
+    # seven multi-tensor passes (~0.2 ms per minibatch at 4,095 envs), the same update rule
+    optimizer = optim.Adam(agent.parameters(), lr=args.learning_rate, eps=1e-5, fused=device.type == "cuda")
     gen = torch.Generator(device=device).manual_seed(seed)
 
     T, E = args.num_steps, args.num_envs

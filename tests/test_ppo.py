@@ -499,3 +499,30 @@ def test_importing_the_train_module_changes_no_environment_variable():
             "assert P.disable_graph_packet_capture() and os.environ['DEBUG_CLR_GRAPH_PACKET_CAPTURE'] == '0'")
     pkg = os.path.dirname(P.__file__)
     subprocess.run([sys.executable, "-c", code.format(pkg=pkg)], check=True, timeout=300)
+
+
+@pytest.mark.gpu
+def test_fused_adam_and_flat_clip_match_reference_optimizer_step_gpu():
+    """train() steps torch's fused Adam on the GPU and clips the flat gradient buffer in one reduction;
+    the reference steps torch's default (multi-tensor) Adam after clip_grad_norm_ over the parameters
+    (ppo…:166, 353).  Same update rule: one update of 2 epochs x 2 minibatches ends within fp32
+    rounding of the reference's (1e-6 relative, 1e-7 absolute)."""
+    args = _args(norm_adv=True, clip_vloss=False)
+    obs, act, logp, adv, ret, val = [t.cuda() for t in _synthetic_batch(5, 32768)]
+    res = []
+    for fused in (False, True):
+        agent = make_agent(2).cuda()
+        flat = P.FlatGrads(agent)
+        opt = torch.optim.Adam(agent.parameters(), lr=1e-3, eps=1e-5, fused=fused)
+        gen = torch.Generator(device="cuda").manual_seed(7)
+        if fused:
+            P.ppo_update(agent, opt, flat, args, obs, logp, act, adv, ret, val, gen=gen)
+        else:  # the reference's clip over the parameters
+            orig = P.FlatGrads.clip_norm_
+            try:
+                P.FlatGrads.clip_norm_ = lambda self, m: torch.nn.utils.clip_grad_norm_(agent.parameters(), m)
+                P.ppo_update(agent, opt, flat, args, obs, logp, act, adv, ret, val, gen=gen)
+            finally:
+                P.FlatGrads.clip_norm_ = orig
+        res.append(torch.cat([p.detach().reshape(-1) for p in agent.parameters()]))
+    torch.testing.assert_close(res[1], res[0], rtol=1e-6, atol=1e-7)

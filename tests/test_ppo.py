@@ -526,3 +526,16 @@ def test_fused_adam_and_flat_clip_match_reference_optimizer_step_gpu():
                 P.FlatGrads.clip_norm_ = orig
         res.append(torch.cat([p.detach().reshape(-1) for p in agent.parameters()]))
     torch.testing.assert_close(res[1], res[0], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_train_amp_bf16_option_gpu(tmp_path):
+    """--amp bf16 (opt-in, not the reference's numerics): the networks under bf16 autocast, the fused
+    loss in fp32, eager update (no captured minibatch): two updates run with finite losses."""
+    args = P.parse_args(["--env-id", "sa", "--num-envs", "4096", "--num-steps", "16", "--update-epochs", "2",
+                         "--num-updates", "2", "--amp", "bf16", "--save-path", str(tmp_path), "--log", "false"])
+    agent, hist = P.train(args)
+    assert len(hist) == 2
+    for h in hist:
+        for k in ("v_loss", "pg_loss", "entropy", "approx_kl"):
+            assert np.isfinite(h[k]), (k, h)

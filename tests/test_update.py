@@ -335,3 +335,27 @@ def test_update_gradients_on_rollout_data_at_fp32_error_gpu():
         ea = float((a - c).norm() / c.norm())
         eb = float((b - c).norm() / c.norm())
         assert ea <= (1.25 if eb >= 1e-6 else 2.0) * eb + 1e-9 and ea < 1e-5, (name, ea, eb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("out_fwd,out_bwd", [(False, True), (True, False), (False, False)])
+def test_output_layer_ab_switches_match_autograd_gpu(out_fwd, out_bwd, monkeypatch):
+    """The A/B switches of _TanhMLP's output layer (VSS_OUTPUT_FWD=0: a separate addmm instead of the
+    folded epilogue; VSS_OUTPUT_BWD=0: the padded backward GEMM + split-K dW instead of the one-pass
+    vss_output_backward) compute the same function and gradients as autograd (fp32 tolerances of
+    test_update_gradients_through_hip_match_autograd_gpu)."""
+    monkeypatch.setattr(P, "OUTPUT_FWD", out_fwd)
+    monkeypatch.setattr(P, "OUTPUT_BWD", out_bwd)
+    agent = make_agent(2).cuda()
+    g = torch.Generator(device="cuda").manual_seed(4)
+    rows = 65536
+    x = torch.randn(rows, 52, device="cuda", generator=g)
+    a = torch.randn(rows, 2, device="cuda", generator=g) * 0.5
+    outs_ref = agent.get_action_and_value(x, a)
+    grads_ref = torch.autograd.grad(outs_ref[1].sum() + outs_ref[3].sum(), list(agent.parameters()))
+    outs = P.get_action_and_value_update(agent, x, a)
+    for u, v in zip(outs[1:], outs_ref[1:]):
+        torch.testing.assert_close(u, v, rtol=2e-5, atol=2e-5)
+    grads = torch.autograd.grad(outs[1].sum() + outs[3].sum(), list(agent.parameters()))
+    for (name, _), u, v in zip(agent.named_parameters(), grads, grads_ref):
+        torch.testing.assert_close(u, v, rtol=2e-4, atol=2e-4 * float(v.abs().max()) + 1e-6, msg=name)

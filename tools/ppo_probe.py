@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Profiling-only: per-update rollout / update times of the SA PPO loop at 65,536 envs, run
+"""Profiling-only: per-update rollout / update times of the PPO loop (ENV_ID sa|cma|dma, NUM_ENVS rows, default SA at 65,536), run
 standalone (PROBE_ENV=0) or after creating a 65,536-field FULL env and stepping it the way
 bench.py does first (PROBE_ENV=1)."""
 import os
@@ -18,7 +18,7 @@ if os.environ.get("PROBE_ENV", "0") == "1":
     for _ in range(300):
         env.step(a)
     torch.cuda.synchronize()
-args = P.parse_args(["--env-id", "sa", "--num-envs", os.environ.get("NUM_ENVS", "65536"), "--num-updates", os.environ.get("UPDATES", "3"),
+args = P.parse_args(["--env-id", os.environ.get("ENV_ID", "sa"), "--num-envs", os.environ.get("NUM_ENVS", "65536"), "--num-updates", os.environ.get("UPDATES", "3"),
                      "--log", os.environ.get("PROBE_LOG", "false"), "--seed", "1", "--save-path", "/tmp/runs"])
 _, hist = P.train(args)
 for h in hist:

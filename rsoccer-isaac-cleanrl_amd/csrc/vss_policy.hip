@@ -410,6 +410,173 @@ __global__ __launch_bounds__(kWaves * 64) void policy_kernel_both(PolicyArgs p) 
   else policy_body<NACT, false>(p, (int64_t)blockIdx.x - half, lds, tails);
 }
 
+// ---- small batches: each pass's 16 output tiles split over the workgroup's 4 waves ---------------------
+// Up to kBothMaxWorkgroups x 64 rows (the reference's 4,095 envs) the kernels above run one wave per 16
+// rows, so only rows / 16 of the 1,024 SIMDs work and each of them multiplies every weight: 4,095 rows
+// keep 512 SIMDs busy for 2,100 MFMAs x 4 per network.  Here a workgroup takes ONE 16-row group and
+// its 4 waves split every pass's 16 tiles (wave w: tiles 4 w .. 4 w + 3 of each pass, i.e. float4 q = w
+// of each k-step block, read straight from L2 -- no staging ring), so each wave runs a quarter of the
+// MFMAs and the row groups x 4 waves fill the chip.  A layer's activations go through LDS: every wave
+// writes its tiles in the B-operand layout h[nt][lane] (lane: row lane & 15, features 16 nt + 4
+// (lane >> 4) + 0..3) and, after one barrier, reads all of them back into registers for the next
+// layer (two buffers, so a wave's writes never meet another wave's reads of the same buffer).  The
+// arithmetic per output -- the k order, the MFMA chain, bias + tanh, the output layer, the sampling tail
+// -- is that of policy_kernel.
+// up to 256 row groups (4,096 rows): actor + critic = 512 workgroups, one pass of two per CU.  Against
+// policy_kernel_both, same bits: 4,095 rows 110 vs 156 us, 1 row 58 vs 149 us; at 8,192 rows (two passes)
+// 206 vs 157 us, so larger batches keep the kernels above (profiles/r04_policy_split_ab.log)
+constexpr int64_t kSplitMaxGroups = 256;
+constexpr int kSplitPrefetch = 4;                   // k-steps of weights in flight per wave
+constexpr int kSplitBuf = (kH2 / 16) * 64;          // f32x4 per activation buffer (512 features: 32 KB)
+
+template <int S, int NUSED, int NP, int KIN>
+__device__ __forceinline__ void split_layer(const f32x4* __restrict__ blocks, const float (&hin)[KIN], f32x4 (&acc)[NP][4],
+                                            int wave, int lane) {
+  // blocks: the layer's first k-step block; pass p, k-step s at block p S + s; this wave's float4 is q = wave
+  const f32x4* src = blocks + wave * 64 + lane;
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[p][c] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  f32x4 w[kSplitPrefetch][NP];
+#pragma unroll
+  for (int s = 0; s < kSplitPrefetch && s < NUSED; ++s)
+#pragma unroll
+    for (int p = 0; p < NP; ++p) w[s][p] = src[(int64_t)(p * S + s) * (kStepFloats / 4)];
+#pragma unroll
+  for (int s = 0; s < NUSED; ++s) {
+    f32x4 cur[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) cur[p] = w[s % kSplitPrefetch][p];
+    if (s + kSplitPrefetch < NUSED) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        w[s % kSplitPrefetch][p] = src[(int64_t)(p * S + s + kSplitPrefetch) * (kStepFloats / 4)];
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[p][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[p][c], hin[s], acc[p][c], 0, 0, 0);
+  }
+}
+
+// bias + tanh of this wave's tiles (pass p, tile 4 wave + c) into the activation buffer, B-operand layout
+template <int NP>
+__device__ __forceinline__ void split_store(const f32x4 (&acc)[NP][4], const float* bias, f32x4* buf, int wave, int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int nt = kTiles * p + 4 * wave + c;
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);  // LDS
+      f32x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fast_tanh(acc[p][c][r] + bb[r]);
+      buf[nt * 64 + lane] = v;
+    }
+}
+
+// all NT tiles of a layer's output back into the B operands of the next layer's k-steps
+template <int NT>
+__device__ __forceinline__ void split_load(const f32x4* buf, int lane, float (&h)[4 * NT]) {
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const f32x4 v = buf[nt * 64 + lane];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) h[4 * nt + r] = v[r];
+  }
+}
+
+template <int NACT, bool ACTOR>
+__device__ __forceinline__ void split_body(const PolicyArgs& p, int64_t grp, f32x4* hb, float* tails) {
+  constexpr int NOUT = ACTOR ? NACT : 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* net = ACTOR ? p.actor : p.critic;
+  const f32x4* stream = reinterpret_cast<const f32x4*>(net);
+  const int64_t r0 = grp * kRowsPerWave;
+  for (int i = threadIdx.x; i < tail_floats(NOUT); i += kWaves * 64) tails[i] = net[off_w5() + i];
+  float x[16];
+  load_rows(p.obs, p.rows, r0, lane, x);
+  __syncthreads();
+  const float* bias = tails + NOUT * kH4;
+  const float *b1 = bias, *b2 = b1 + kH1, *b3 = b2 + kH2, *b4 = b3 + kH3;
+  f32x4* buf0 = hb;
+  f32x4* buf1 = hb + kSplitBuf;
+  {
+    f32x4 acc[1][4];
+    split_layer<kStepsL1, kUsedStepsL1, 1, 16>(stream, x, acc, wave, lane);
+    split_store<1>(acc, b1, buf0, wave, lane);
+  }
+  __syncthreads();
+  {
+    float h[kH1 / 4];
+    split_load<kH1 / 16>(buf0, lane, h);
+    f32x4 acc[2][4];
+    split_layer<kStepsL2, kStepsL2, 2, kH1 / 4>(stream + (int64_t)kStepsL1 * (kStepFloats / 4), h, acc, wave, lane);
+    split_store<2>(acc, b2, buf1, wave, lane);
+  }
+  __syncthreads();
+  {
+    float h[kH2 / 4];
+    split_load<kH2 / 16>(buf1, lane, h);
+    f32x4 acc[2][4];
+    split_layer<kStepsL3, kStepsL3, 2, kH2 / 4>(stream + (int64_t)(kStepsL1 + 2 * kStepsL2) * (kStepFloats / 4), h, acc,
+                                                wave, lane);
+    split_store<2>(acc, b3, buf0, wave, lane);
+  }
+  __syncthreads();
+  {
+    float h[kH3 / 4];
+    split_load<kH3 / 16>(buf0, lane, h);
+    f32x4 acc[1][4];
+    split_layer<kStepsL4, kStepsL4, 1, kH3 / 4>(
+        stream + (int64_t)(kStepsL1 + 2 * kStepsL2 + 2 * kStepsL3) * (kStepFloats / 4), h, acc, wave, lane);
+    split_store<1>(acc, b4, buf1, wave, lane);
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  // the output layer and the tail as mlp() / policy_body do, on wave 0
+  float h4[kH4 / 4];
+  split_load<kH4 / 16>(buf1, lane, h4);
+  const int g = lane >> 4;
+  float out[NOUT];
+#pragma unroll
+  for (int a = 0; a < NOUT; ++a) {
+    const f32x4* w = reinterpret_cast<const f32x4*>(tails + a * kH4 + 64 * g);
+    float acc = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const f32x4 ww = w[t];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc += ww[r] * h4[4 * t + r];
+    }
+    acc += __shfl_xor(acc, 16);
+    acc += __shfl_xor(acc, 32);
+    out[a] = acc + bias[kH1 + kH2 + kH3 + kH4 + a];
+  }
+  const int64_t row = r0 + (lane & 15);
+  const bool writer = g == 0 && row < p.rows;
+  if constexpr (ACTOR) {
+    if (writer)
+      actor_tail<NACT>(out, row, p.logstd, p.seed, p.counter, p.action_in, p.action_out, p.logprob_out, p.entropy_out,
+                       p.mean_out);
+  } else {
+    if (writer && p.value_out) p.value_out[row] = out[0];
+  }
+}
+
+// actor and critic of every 16-row group in one launch: blocks [0, groups) the actor, [groups, 2 groups)
+// the critic; 2 workgroups per CU (LDS: two 32-KB activation buffers + the packed tail)
+template <int NACT>
+__global__ __launch_bounds__(kWaves * 64, 2) void policy_split_kernel(PolicyArgs p) {
+  __shared__ __attribute__((aligned(16))) f32x4 hb[2 * kSplitBuf];
+  __shared__ __attribute__((aligned(16))) float tails[tail_floats(NACT)];
+  const int64_t groups = gridDim.x / 2;
+  if ((int64_t)blockIdx.x < groups) split_body<NACT, true>(p, blockIdx.x, hb, tails);
+  else split_body<NACT, false>(p, (int64_t)blockIdx.x - groups, hb, tails);
+}
+
 }  // namespace vpol
 
 extern "C" {
@@ -455,7 +622,14 @@ int vss_value_forward_masked(void* stream, int64_t rows, int32_t n_act, const fl
   const int64_t wgs = (waves + vpol::kWaves - 1) / vpol::kWaves;
   const dim3 grid((unsigned)wgs), block(vpol::kWaves * 64);
   hipStream_t s = (hipStream_t)stream;
-  if (!critic_only && wgs <= vpol::kBothMaxWorkgroups) {  // small batch: both networks in one launch
+  if (!critic_only && waves <= vpol::kSplitMaxGroups) {
+    // small batch: both networks in one launch, one workgroup per 16-row group, tiles split over its waves
+    const dim3 grid2((unsigned)(2 * waves));
+    if (n_act == 2) hipLaunchKernelGGL((vpol::policy_split_kernel<2>), grid2, block, 0, s, a);
+    else hipLaunchKernelGGL((vpol::policy_split_kernel<6>), grid2, block, 0, s, a);
+    return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+  }
+  if (!critic_only && wgs <= vpol::kBothMaxWorkgroups) {  // both networks in one launch
     const dim3 grid2((unsigned)(2 * wgs));
     if (n_act == 2) hipLaunchKernelGGL((vpol::policy_kernel_both<2>), grid2, block, 0, s, a);
     else hipLaunchKernelGGL((vpol::policy_kernel_both<6>), grid2, block, 0, s, a);

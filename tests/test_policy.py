@@ -29,7 +29,9 @@ def make_agent(act_dim, seed):
     return a
 
 
-@pytest.mark.parametrize("act_dim,rows", [(2, 65536), (6, 4096), (2, 1), (2, 37), (6, 1000)])
+# rows <= 4,096: policy_split_kernel (one 16-row group per workgroup, tiles split over its waves);
+# 4,097-8,192: policy_kernel_both; larger: one launch per network (the rollout's chain path aside)
+@pytest.mark.parametrize("act_dim,rows", [(2, 65536), (6, 4096), (2, 1), (2, 37), (6, 1000), (2, 4097), (6, 8192)])
 def test_fused_forward_matches_agent(act_dim, rows):
     from vss_amd.policy import FusedPolicy
     agent = make_agent(act_dim, 7 + act_dim)

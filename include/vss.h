@@ -340,6 +340,16 @@ int vss_output_backward(void* stream, int64_t rows, int32_t k_pad, int32_t n, co
  * vss_linear_tanh_backward_chunks_bf16x6 parts.  w_split: caller-owned scratch of 3 * n_out * k
  * uint16 (16-B aligned) that the call fills with the weight's bf16 planes before its GEMM reads them.
  *
+ * w (resp. w_next_t) == NULL: w_split already holds the weight's planes, written by
+ * vss_weight_planes_bf16x6 for this (n_out, k) since the weight last changed (no split launch).
+ *
+ * vss_weight_planes_bf16x6: the planes of `count` (1..8) weights in ONE launch, into the w_split
+ * buffers the GEMM entries above then take with a NULL weight: job q is an (n[q], k[q]) operand
+ * (n % 128 == 0, n <= 4096, k % 64 == 0), stored row-major as w[q] (n, k) when transpose[q] == 0, or
+ * as its transpose (k, n) when transpose[q] == 1 (the backward's W_next^T straight from nn.Linear's
+ * weight, no transposed copy).  Host arrays of `count` entries; w_split 16-B aligned, w 16-B
+ * aligned when not transposed.  Replaces one split launch per GEMM and the backward's transposes.
+ *
  * vss_weight_grad_bf16x6: a Linear layer's weight gradient (autograd of nn.Linear, ppo…:357)
  *   partial[s][o][i] = sum over the rows r of part s of grad[r][o] x[r][i]
  * grad (rows, n_out) = the layer's output gradient, x (rows, k_in) = its input; dW = the sum over the
@@ -356,6 +366,8 @@ int64_t vss_linear_tanh_backward_chunks_bf16x6(int64_t rows, int32_t k_next, int
 int vss_linear_tanh_backward_bf16x6(void* stream, int64_t rows, int32_t k_next, int32_t n_out, const float* grad_next,
                                     const float* w_next_t, const float* y, float* grad_in, float* bias_partial,
                                     uint16_t* w_split);
+int vss_weight_planes_bf16x6(void* stream, int32_t count, const float* const* w, const int32_t* n, const int32_t* k,
+                             const int32_t* transpose, uint16_t* const* w_split);
 int64_t vss_weight_grad_chunks_bf16x6(int64_t rows, int32_t n_out, int32_t k_in);
 int vss_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_in, const float* grad, const float* x,
                            float* partial);

@@ -297,6 +297,50 @@ __global__ __launch_bounds__(256) void split_image_kernel(const float* __restric
   *reinterpret_cast<u32x4*>(d + 2 * 4 * R * 8) = lo;
 }
 
+// several weights' plane images in one launch (vss_weight_planes_bf16x6): job blockIdx.y, the same image
+// bytes as split_image_kernel<r>; `trans` = the job's fp32 weight is stored (k, n), i.e. the image is
+// of its transpose (the backward's W_next^T, without a transposed copy)
+struct PlaneJob {
+  const float* w;
+  uint16_t* img;
+  int64_t n, k;
+  int32_t trans, r;
+};
+constexpr int kMaxPlaneJobs = 8;
+struct PlaneJobs {
+  PlaneJob j[kMaxPlaneJobs];
+};
+
+__global__ __launch_bounds__(256) void plane_images_kernel(PlaneJobs jobs) {
+  const PlaneJob& J = jobs.j[blockIdx.y];
+  const int64_t ktn = J.k / KT, units = J.n * J.k / 8;
+  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (it, kt, g, r), r fastest
+  if (u >= units) return;
+  const int R = J.r;
+  const int r = (int)(u % R), g = (int)((u / R) % 4);
+  const int64_t kt = (u / (4 * R)) % ktn, it = u / (4 * R * ktn);
+  const int64_t row = it * R + r, col = kt * KT + 8 * g;  // element (row, col .. col + 7) of the (n, k) operand
+  float v[8];
+  if (J.trans) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = J.w[(col + e) * J.n + row];  // lanes r: consecutive words of one row of w
+  } else {
+    const u32x4 a = *reinterpret_cast<const u32x4*>(J.w + row * J.k + col);
+    const u32x4 b = *reinterpret_cast<const u32x4*>(J.w + row * J.k + col + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = __uint_as_float(a[e]);
+      v[4 + e] = __uint_as_float(b[e]);
+    }
+  }
+  u32x4 hi, mid, lo;
+  split8(v, hi, mid, lo);
+  uint16_t* d = J.img + (it * ktn + kt) * (3 * 4 * (int64_t)R * 8) + ((int64_t)g * R + r) * 8;
+  *reinterpret_cast<u32x4*>(d) = hi;
+  *reinterpret_cast<u32x4*>(d + 4 * R * 8) = mid;
+  *reinterpret_cast<u32x4*>(d + 2 * 4 * R * 8) = lo;
+}
+
 // sum over the 16 lanes of a DPP row (as vss_update.hip row16_sum)
 template <int CTRL>
 __device__ __forceinline__ float dpp_f32(float x) {
@@ -704,10 +748,10 @@ int vss_linear_tanh_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_o
   using namespace vx6;
   return with_fb_cfg(n_out, [&](auto cfg) {
     using C = decltype(cfg);
-    if (!fb_shape_ok<C>(rows, k_in, n_out) || misaligned(x) || misaligned(w) || misaligned(y) || !bias ||
+    if (!fb_shape_ok<C>(rows, k_in, n_out) || (w && misaligned(w)) || misaligned(x) || misaligned(y) || !bias ||
         misaligned(w_split))
       return (int)VSS_E_ARG;
-    int rc = split_weight<C>(stream, w, n_out, k_in, w_split);
+    int rc = w ? split_weight<C>(stream, w, n_out, k_in, w_split) : VSS_OK;
     if (rc != VSS_OK) return rc;
     Args a = fb_args(k_in, n_out, w_split, x, y);
     a.bias = bias;
@@ -721,10 +765,10 @@ int vss_linear_tanh_out_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t
   using namespace vx6;
   return with_fb_cfg(n_out, [&](auto cfg) {
     using C = decltype(cfg);
-    if (!fb_shape_ok<C>(rows, k_in, n_out) || n_out != 256 || misaligned(x) || misaligned(w) || misaligned(y) ||
+    if (!fb_shape_ok<C>(rows, k_in, n_out) || n_out != 256 || misaligned(x) || (w && misaligned(w)) || misaligned(y) ||
         !bias || !w_out || !out_part || !(k_out == 1 || k_out == 2 || k_out == 6) || misaligned(w_split))
       return (int)VSS_E_ARG;
-    int rc = split_weight<C>(stream, w, n_out, k_in, w_split);
+    int rc = w ? split_weight<C>(stream, w, n_out, k_in, w_split) : VSS_OK;
     if (rc != VSS_OK) return rc;
     Args a = fb_args(k_in, n_out, w_split, x, y);
     a.bias = bias;
@@ -753,16 +797,38 @@ int vss_linear_tanh_backward_bf16x6(void* stream, int64_t rows, int32_t k_next, 
   using namespace vx6;
   return with_fb_cfg(n_out, [&](auto cfg) {
     using C = decltype(cfg);
-    if (!fb_shape_ok<C>(rows, k_next, n_out) || misaligned(grad_next) || misaligned(w_next_t) || misaligned(y) ||
-        misaligned(grad_in) || misaligned(bias_partial) || misaligned(w_split))
+    if (!fb_shape_ok<C>(rows, k_next, n_out) || misaligned(grad_next) || (w_next_t && misaligned(w_next_t)) ||
+        misaligned(y) || misaligned(grad_in) || misaligned(bias_partial) || misaligned(w_split))
       return (int)VSS_E_ARG;
-    int rc = split_weight<C>(stream, w_next_t, n_out, k_next, w_split);
+    int rc = w_next_t ? split_weight<C>(stream, w_next_t, n_out, k_next, w_split) : VSS_OK;
     if (rc != VSS_OK) return rc;
     Args a = fb_args(k_next, n_out, w_split, grad_next, grad_in);
     a.y = y;
     a.partial = bias_partial;
     return launch<EPI_DTANH, ST_DMA, ST_ROW, C>(stream, a, fb_plan<C>(rows, k_next, n_out));
   });
+}
+
+int vss_weight_planes_bf16x6(void* stream, int32_t count, const float* const* w, const int32_t* n, const int32_t* k,
+                             const int32_t* transpose, uint16_t* const* w_split) {
+  using namespace vx6;
+  if (count < 1 || count > kMaxPlaneJobs || !w || !n || !k || !transpose || !w_split) return VSS_E_ARG;
+  PlaneJobs jobs{};
+  int64_t blocks = 0;
+  for (int q = 0; q < count; ++q) {
+    const int32_t nq = n[q], kq = k[q];
+    // the image's row tile is the forward / backward block's (with_fb_cfg): 256 where n % 256 == 0
+    if (nq <= 0 || nq % CfgA::BI || nq > 4096 || kq <= 0 || kq % (2 * KT) || kq > 65536 || !w[q] ||
+        misaligned(w_split[q]) || (transpose[q] != 0 && transpose[q] != 1) ||
+        (!transpose[q] && misaligned(w[q])))
+      return VSS_E_ARG;
+    jobs.j[q] = PlaneJob{w[q], w_split[q], nq, kq, transpose[q], nq % CfgB::BI == 0 ? CfgB::BI : CfgA::BI};
+    const int64_t b = ((int64_t)nq * kq / 8 + 255) / 256;
+    if (b > blocks) blocks = b;
+  }
+  hipLaunchKernelGGL(plane_images_kernel, dim3((unsigned)blocks, (unsigned)count), dim3(256), 0, (hipStream_t)stream,
+                     jobs);
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 
 int64_t vss_weight_grad_chunks_bf16x6(int64_t rows, int32_t n_out, int32_t k_in) {

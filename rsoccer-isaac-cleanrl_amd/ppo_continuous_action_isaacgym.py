@@ -58,7 +58,8 @@ from envs._gym import Box, ObservationWrapper  # noqa: E402
 from vss_amd.loss import ppo_loss  # noqa: E402
 from vss_amd.update import (gemm_shape_ok, linear_tanh, linear_tanh_backward, linear_tanh_backward_mixed,  # noqa: E402
                             linear_tanh_mixed, linear_tanh_out, linear_tanh_out_mixed, linear_tanh_out_ok,
-                            output_backward, output_backward_ok, tanh_grad_bias, weight_grad_mixed)
+                            output_backward, output_backward_ok, tanh_grad_bias, weight_grad_mixed, weight_planes,
+                            x6_ok)
 
 
 def strtobool(x: str) -> bool:
@@ -191,15 +192,15 @@ class _LinearSplitK(torch.autograd.Function):
         return gx, _split_k_wgrad(gy, x), gy.sum(0)
 
 
-def _split_k_wgrad(gz, x):
+def _split_k_wgrad(gz, x, out=None):
     rows = x.shape[0]
     if rows >= SPLITK_MIN_ROWS:
         # the rows in SPLITK equal chunks (one batched GEMM + a sum), the < SPLITK left over added
         main = rows // SPLITK * SPLITK
-        dw = torch.bmm(gz[:main].reshape(SPLITK, main // SPLITK, gz.shape[1]).transpose(1, 2),
-                       x[:main].reshape(SPLITK, main // SPLITK, x.shape[1])).sum(0)
+        dw = torch.sum(torch.bmm(gz[:main].reshape(SPLITK, main // SPLITK, gz.shape[1]).transpose(1, 2),
+                                 x[:main].reshape(SPLITK, main // SPLITK, x.shape[1])), 0, out=out)
         return dw.addmm_(gz[main:].t(), x[main:]) if main < rows else dw
-    return gz.t().mm(x)
+    return torch.mm(gz.t(), x, out=out)
 
 
 class _LinearTanh(torch.autograd.Function):
@@ -236,15 +237,21 @@ class _TanhMLP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, *params):
         ws, bs = params[0::2], params[1::2]
+        ctx.params = params  # the backward writes the FlatGrads-owned gradients in place (_grad_dst)
         hs = [x]
         rows = x.shape[0]
         x6 = x.is_cuda and UPDATE_GEMM == "x6"
-        for w, b in zip(ws[:-2], bs[:-2]):
-            hs.append((linear_tanh_mixed if x6 else linear_tanh)(hs[-1], w, b))
+        # the x6 layers' weight planes, forward (W) and backward (W^T), in one launch for the whole MLP
+        pf, ctx.planes_b = _mlp_planes(ws, rows) if x6 and WEIGHT_PLANES else ({}, {})
+        for layer, (w, b) in enumerate(zip(ws[:-2], bs[:-2])):
+            if x6:
+                hs.append(linear_tanh_mixed(hs[-1], w, b, planes=pf.get(layer)))
+            else:
+                hs.append(linear_tanh(hs[-1], w, b))
         if x6 and OUTPUT_FWD:
             # the last hidden layer and the output layer in one launch per row range (the whole 256-row
             # tiles through vss_linear_tanh_out_bf16x6, the rest through vss_linear_tanh + addmm)
-            h, out = linear_tanh_out_mixed(hs[-1], ws[-2], bs[-2], ws[-1], bs[-1])
+            h, out = linear_tanh_out_mixed(hs[-1], ws[-2], bs[-2], ws[-1], bs[-1], planes=pf.get(len(ws) - 2))
             hs.append(h)
         elif x.is_cuda and OUTPUT_FWD and linear_tanh_out_ok(rows, ws[-2].shape[1], ws[-2].shape[0], ws[-1].shape[0]):
             # the last hidden layer and the output layer in one launch (vss_linear_tanh_out)
@@ -262,20 +269,22 @@ class _TanhMLP(torch.autograd.Function):
         n = len(saved) // 2
         hs, ws = saved[:n], saved[n:]  # hs[l] = input of layer l (hs[0] = x), ws[l] = its weight
         grads = [None] * (2 * n)
+        dst = [_grad_dst(p) if gout.is_cuda else None for p in ctx.params]
         gz = gout.contiguous()  # pre-activation gradient of the current layer
-        gb = gz.sum(0)
+        gb = torch.sum(gz, 0, out=dst[2 * n - 1])
         for layer in reversed(range(n)):
             if OUTPUT_BWD and layer == n - 1 and layer > 0 and output_backward_ok(gz.shape[1], hs[layer].shape[1]):
                 # the output layer (1-6 columns): its weight gradient and the backward into the tanh
                 # layer below in one streaming pass over that layer's output (vss_output_backward)
                 grads[2 * layer + 1] = gb
-                gz, gb, grads[2 * layer] = output_backward(gz, ws[layer], hs[layer])
+                gz, gb, grads[2 * layer] = output_backward(gz, ws[layer], hs[layer], out_db=dst[2 * layer - 1],
+                                                           out_dw=dst[2 * layer])
                 continue
             x6 = gz.is_cuda and UPDATE_GEMM == "x6"
             if x6 and hs[layer].shape[1] % 128 == 0 and gz.shape[1] % 256 == 0:
-                grads[2 * layer] = weight_grad_mixed(gz, hs[layer])
+                grads[2 * layer] = weight_grad_mixed(gz, hs[layer], out=dst[2 * layer])
             else:
-                grads[2 * layer] = _split_k_wgrad(gz, hs[layer])
+                grads[2 * layer] = _split_k_wgrad(gz, hs[layer], out=dst[2 * layer])
             grads[2 * layer + 1] = gb
             if layer == 0:
                 break
@@ -285,10 +294,44 @@ class _TanhMLP(torch.autograd.Function):
                 # GEMM's contraction granule, so this backward is one fused pass as well
                 pad = 4 - gz.shape[1] % 4
                 gz, w = nn.functional.pad(gz, (0, pad)), nn.functional.pad(w, (0, 0, 0, pad))
-            gz, gb = (linear_tanh_backward_mixed if x6 else linear_tanh_backward)(gz, w, hs[layer])
+            if x6:
+                gz, gb = linear_tanh_backward_mixed(gz, w, hs[layer], out_db=dst[2 * layer - 1],
+                                                    planes=ctx.planes_b.get(layer) if layer < n - 1 else None)
+            else:
+                gz, gb = linear_tanh_backward(gz, w, hs[layer])
+                if dst[2 * layer - 1] is not None:
+                    gb = dst[2 * layer - 1].copy_(gb)
         gx = gz.mm(ws[0]) if ctx.needs_input_grad[0] else None
-        return (gx, *grads)
+        # the gradients already written into their parameters' .grad are not handed to autograd
+        # (whose AccumulateGrad would add them to themselves)
+        return (gx, *[None if d is not None else g for g, d in zip(grads, dst)])
 
+
+def _mlp_planes(ws, rows: int):
+    """The bf16 planes of the hidden layers' weights the x6 GEMMs take (vss_weight_planes_bf16x6, one
+    launch): {layer: planes of W} for the forwards of layers 1 .. L-2 and {layer: planes of W^T} for
+    their backwards (layer 0's input width is the observation's, below the x6 shapes; layer L-1 is the
+    output layer).  Valid for this minibatch: the weights change only at the optimizer step."""
+    if rows < 256:
+        return {}, {}
+    jobs = []
+    for layer in range(1, len(ws) - 1):
+        n, k = ws[layer].shape
+        if x6_ok(256, k, n):
+            jobs.append((layer, False))
+        if x6_ok(256, n, k):
+            jobs.append((layer, True))
+    if not jobs:
+        return {}, {}
+    planes = weight_planes([(ws[layer], tr) for layer, tr in jobs])
+    pf = {layer: p for (layer, tr), p in zip(jobs, planes) if not tr}
+    pb = {layer: p for (layer, tr), p in zip(jobs, planes) if tr}
+    return pf, pb
+
+
+# the x6 weights' planes: "1" (default) = one vss_weight_planes_bf16x6 launch per MLP and minibatch
+# (forward W and backward W^T), "0" = each GEMM entry splits (and the backward transposes) its weight
+WEIGHT_PLANES = os.environ.get("VSS_WEIGHT_PLANES", "1") == "1"
 
 # the update's MLP path: "fused" (default) = _TanhMLP (our fp32 MFMA GEMMs with the tanh work in
 # their epilogues: 3.51 s per SA update at 65,536 envs); "split" = _LinearTanh / _LinearSplitK
@@ -359,9 +402,25 @@ class ExtractObsWrapper(ObservationWrapper):
         return obs["obs"]
 
 
+_DIRECT_GRADS = [False]  # set by FlatGrads.zeroed_backward() around the update's loss.backward()
+
+
+def _grad_dst(p: torch.Tensor):
+    """The .grad of a FlatGrads-owned parameter, which _TanhMLP's backward writes directly inside
+    FlatGrads.zeroed_backward(): the buffer was zeroed just before and each parameter receives exactly
+    one gradient per backward, so writing it equals autograd's accumulation into zero -- without one add
+    kernel per parameter.  None anywhere else (plain autograd: torch.autograd.grad, other callers)."""
+    g = p.grad
+    if _DIRECT_GRADS[0] and getattr(p, "_vss_flat_grad", False) and g is not None and g.is_cuda \
+            and g.dtype == torch.float32:
+        return g
+    return None
+
+
 class FlatGrads:
     """All parameter gradients as views of ONE contiguous fp32 buffer, so the data-parallel
-    exchange is a single all-reduce (4.3 MB for the SA agent) with no pack/unpack copies."""
+    exchange is a single all-reduce (4.3 MB for the SA agent) with no pack/unpack copies.  The MLPs'
+    backward (_TanhMLP) writes their gradients straight into these views (_grad_dst)."""
 
     def __init__(self, module: nn.Module):
         self.params = [p for p in module.parameters() if p.requires_grad]
@@ -370,10 +429,20 @@ class FlatGrads:
         off = 0
         for p in self.params:
             p.grad = self.flat[off:off + p.numel()].view_as(p)
+            p._vss_flat_grad = True
             off += p.numel()
 
     def zero(self):
         self.flat.zero_()
+
+    def zeroed_backward(self, loss: torch.Tensor):
+        """zero() then loss.backward() (ppo…:351-352), the MLPs' gradients written in place (_grad_dst)."""
+        self.zero()
+        _DIRECT_GRADS[0] = True
+        try:
+            loss.backward()
+        finally:
+            _DIRECT_GRADS[0] = False
 
     def all_reduce_mean(self, world: int):
         if world > 1:
@@ -592,10 +661,9 @@ class MinibatchGraph:
         self.failed = False  # a self-check found the replay differing from eager: eager from then on
 
     def _body(self):
-        self.flat.zero()
         loss, st = minibatch_losses(self.agent, self.args, self.obs, self.act, self.logp, self.adv, self.ret,
                                     self.val)
-        loss.backward()
+        self.flat.zeroed_backward(loss)
         # detached: no autograd graph (and no AccumulateGrad node bound to this stream) outlives the step
         return tuple(t.detach() for t in st)
 
@@ -697,10 +765,9 @@ def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_adv
             if graph is not None:
                 st = graph.run(mb_inds, inds_pad, b_obs, b_actions, b_logprobs, mb_adv, b_returns, b_values)
             else:
-                flat.zero()
                 loss, st = minibatch_losses(agent, args, b_obs[inds_pad], b_actions[inds_pad], b_logprobs[mb_inds],
                                             mb_adv, b_returns[mb_inds], b_values[mb_inds])
-                loss.backward()
+                flat.zeroed_backward(loss)
             pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac = st
             clipfracs.append(clipfrac.clone())  # (a graph's outputs are rewritten by the next replay)
             flat.all_reduce_mean(world)  # the data-parallel exchange (RCCL on ROCm)

@@ -148,11 +148,12 @@ def output_backward_ok(k_out: int, n: int) -> bool:
     return 1 <= k_out <= 8 and n >= 128 and n % 128 == 0 and 1024 % n == 0
 
 
-def output_backward(g_out: torch.Tensor, w_out: torch.Tensor, y: torch.Tensor):
+def output_backward(g_out: torch.Tensor, w_out: torch.Tensor, y: torch.Tensor, out_db: torch.Tensor | None = None,
+                    out_dw: torch.Tensor | None = None):
     """Backward through the output nn.Linear (weight w_out (k_out, n)) into the tanh layer below it
     (output y (rows, n), also the output layer's input), g_out (rows, k_out) the output's gradient:
     gz = (g_out @ w_out) * (1 - y^2), db = gz.sum(0) and dw = g_out.T @ y (the output layer's weight
-    gradient)."""
+    gradient).  out_db / out_dw: where to reduce db / dw into (ROCm path; the same tensors returned)."""
     if g_out.dim() != 2 or w_out.dim() != 2 or y.dim() != 2 or g_out.shape[0] != y.shape[0] \
             or w_out.shape != (g_out.shape[1], y.shape[1]):
         raise ValueError(f"output_backward: g_out {tuple(g_out.shape)}, w_out {tuple(w_out.shape)}, y {tuple(y.shape)}")
@@ -179,7 +180,7 @@ def output_backward(g_out: torch.Tensor, w_out: torch.Tensor, y: torch.Tensor):
     N.check(lib.vss_output_backward(N.stream_of(y.device), rows, k_pad, n, g_pad.data_ptr(), w_t.data_ptr(),
                                     y.data_ptr(), gz.data_ptr(), bpart.data_ptr(), wpart.data_ptr()),
             "vss_output_backward")
-    return gz, bpart.sum(0), wpart.sum(0)[:k_out]
+    return gz, torch.sum(bpart, 0, out=out_db), torch.sum(wpart[:, :k_out], 0, out=out_dw)
 
 
 # ---- the same GEMMs in fp32 arithmetic on the bf16 matrix cores (csrc/vss_gemm_x6.hip) ----------------
@@ -203,6 +204,32 @@ def _planes(w: torch.Tensor) -> torch.Tensor:
     return torch.empty((3, w.numel()), device=w.device, dtype=torch.int16)
 
 
+def weight_planes(jobs) -> list:
+    """The bf16 planes of several weights in ONE launch (vss_weight_planes_bf16x6): jobs = [(w, transpose)]
+    with w an fp32 (n, k) weight (transpose False: the forward's P operand) or a (k, n) one whose
+    transpose is the operand (True: the backward's W_next^T, no transposed copy); at most 8.  Returns
+    the planes, to be handed to linear_tanh_x6 / linear_tanh_out_x6 / linear_tanh_backward_x6 (planes=),
+    valid until the weights change."""
+    if not 1 <= len(jobs) <= 8:
+        raise ValueError(f"weight_planes: 1..8 weights per launch, got {len(jobs)}")
+    import ctypes
+    ws, ns, ks, ts, outs = [], [], [], [], []
+    for w, tr in jobs:
+        if w.dim() != 2 or w.dtype != torch.float32 or not w.is_cuda or not w.is_contiguous():
+            raise ValueError(f"weight_planes: contiguous fp32 ROCm (rows, cols) weights, got {w.dtype} {tuple(w.shape)}")
+        n, k = (w.shape[1], w.shape[0]) if tr else (w.shape[0], w.shape[1])
+        ws.append(w.data_ptr())
+        ns.append(n)
+        ks.append(k)
+        ts.append(int(bool(tr)))
+        outs.append(_planes(w))
+    c = len(jobs)
+    P, I = ctypes.c_void_p * c, ctypes.c_int32 * c
+    N.check(N.load().vss_weight_planes_bf16x6(N.stream_of(jobs[0][0].device), c, P(*ws), I(*ns), I(*ks), I(*ts),
+                                              P(*[o.data_ptr() for o in outs])), "vss_weight_planes_bf16x6")
+    return outs
+
+
 def _x6_check(name, cond, *ts):
     if not cond:
         raise ValueError(f"{name}: shape outside the bf16x6 kernels' exact shapes: {[tuple(t.shape) for t in ts]}")
@@ -212,21 +239,33 @@ def _x6_check(name, cond, *ts):
             raise ValueError(f"{name}: ROCm tensors only (no CPU path)")
 
 
-def linear_tanh_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """linear_tanh on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_bf16x6)."""
+def _w_and_planes(w: torch.Tensor, planes: torch.Tensor | None):
+    """(weight pointer, planes pointer) for an x6 entry: the entry splits w itself (planes None), or
+    takes the weight_planes() result with a NULL weight."""
+    if planes is None:
+        return w.data_ptr(), _planes(w).data_ptr()
+    if planes.dtype != torch.int16 or planes.numel() != 3 * w.numel():
+        raise ValueError(f"planes: weight_planes() output of this weight, got {planes.dtype} {tuple(planes.shape)}")
+    return None, planes.data_ptr()
+
+
+def linear_tanh_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
+                   planes: torch.Tensor | None = None) -> torch.Tensor:
+    """linear_tanh on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_bf16x6); planes: w's
+    weight_planes() (transpose False), or None to split w in the call."""
     rows, k = x.shape
     n = w.shape[0]
     _x6_check("vss_linear_tanh_bf16x6", w.shape == (n, k) and b.shape == (n,) and x6_ok(rows, k, n), x, w, b)
     x, w, b = x.contiguous(), w.contiguous(), b.contiguous()
     y = _out(out, (rows, n), x)
-    N.check(N.load().vss_linear_tanh_bf16x6(N.stream_of(x.device), rows, k, n, x.data_ptr(), w.data_ptr(),
-                                            b.data_ptr(), y.data_ptr(), _planes(w).data_ptr()),
-            "vss_linear_tanh_bf16x6")
+    wp, pp = _w_and_planes(w, planes)
+    N.check(N.load().vss_linear_tanh_bf16x6(N.stream_of(x.device), rows, k, n, x.data_ptr(), wp,
+                                            b.data_ptr(), y.data_ptr(), pp), "vss_linear_tanh_bf16x6")
     return y
 
 
 def linear_tanh_out_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out: torch.Tensor, b_out: torch.Tensor,
-                       out: torch.Tensor | None = None):
+                       out: torch.Tensor | None = None, planes: torch.Tensor | None = None):
     """linear_tanh_out on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_out_bf16x6)."""
     rows, k = x.shape
     n, k_out = w.shape[0], w_out.shape[0]
@@ -235,34 +274,41 @@ def linear_tanh_out_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out:
     x, w, b, w_out = x.contiguous(), w.contiguous(), b.contiguous(), w_out.contiguous()
     y = _out(out, (rows, n), x)
     part = torch.empty((n // 64, rows, k_out), device=x.device, dtype=torch.float32)
-    N.check(N.load().vss_linear_tanh_out_bf16x6(N.stream_of(x.device), rows, k, n, x.data_ptr(), w.data_ptr(),
+    wp, pp = _w_and_planes(w, planes)
+    N.check(N.load().vss_linear_tanh_out_bf16x6(N.stream_of(x.device), rows, k, n, x.data_ptr(), wp,
                                                 b.data_ptr(), y.data_ptr(), k_out, w_out.data_ptr(), part.data_ptr(),
-                                                _planes(w).data_ptr()), "vss_linear_tanh_out_bf16x6")
+                                                pp), "vss_linear_tanh_out_bf16x6")
     return y, part.sum(0).add_(b_out)
 
 
 def linear_tanh_backward_x6(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.Tensor,
-                            out: torch.Tensor | None = None):
-    """linear_tanh_backward on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_backward_bf16x6)."""
+                            out: torch.Tensor | None = None, out_db: torch.Tensor | None = None,
+                            planes: torch.Tensor | None = None):
+    """linear_tanh_backward on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_backward_bf16x6);
+    planes: w_next's weight_planes() with transpose True, or None to transpose and split it in the call."""
     rows, k_next = gz_next.shape
     n = y.shape[1]
     _x6_check("vss_linear_tanh_backward_bf16x6", w_next.shape == (k_next, n) and y.shape[0] == rows
               and x6_ok(rows, k_next, n), gz_next, w_next, y)
     lib = N.load()
     gz_next, y = gz_next.contiguous(), y.contiguous()
-    w_t = w_next.t().contiguous()  # (n, k_next): K-contiguous
+    if planes is None:
+        wp, pp = _w_and_planes(w_next.t().contiguous(), None)  # (n, k_next): K-contiguous
+    else:
+        wp, pp = _w_and_planes(w_next, planes)
     gz = _out(out, (rows, n), y)
     partial = torch.empty((lib.vss_linear_tanh_backward_chunks_bf16x6(rows, k_next, n), n), device=y.device,
                           dtype=torch.float32)
     N.check(lib.vss_linear_tanh_backward_bf16x6(N.stream_of(y.device), rows, k_next, n, gz_next.data_ptr(),
-                                                w_t.data_ptr(), y.data_ptr(), gz.data_ptr(), partial.data_ptr(),
-                                                _planes(w_t).data_ptr()), "vss_linear_tanh_backward_bf16x6")
-    return gz, partial.sum(0)
+                                                wp, y.data_ptr(), gz.data_ptr(), partial.data_ptr(), pp),
+            "vss_linear_tanh_backward_bf16x6")
+    return gz, torch.sum(partial, 0, out=out_db)
 
 
-def weight_grad_x6(grad: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+def weight_grad_x6(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """dW = grad.T @ x (a Linear layer's weight gradient, grad (rows, n_out), x (rows, k_in)) on the
-    bf16 matrix cores with fp32 arithmetic, split over the rows (vss_weight_grad_bf16x6)."""
+    bf16 matrix cores with fp32 arithmetic, split over the rows (vss_weight_grad_bf16x6); the parts are
+    reduced into `out` when given."""
     rows, n_out = grad.shape
     k_in = x.shape[1]
     _x6_check("vss_weight_grad_bf16x6", x.shape[0] == rows and x6_wgrad_ok(rows, n_out, k_in), grad, x)
@@ -272,7 +318,7 @@ def weight_grad_x6(grad: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
                         dtype=torch.float32)
     N.check(lib.vss_weight_grad_bf16x6(N.stream_of(x.device), rows, n_out, k_in, grad.data_ptr(), x.data_ptr(),
                                        parts.data_ptr()), "vss_weight_grad_bf16x6")
-    return parts.sum(0)
+    return torch.sum(parts, 0, out=out)
 
 
 # ---- any row count: whole tiles on the bf16x6 kernels, the ragged rest on the fp32 ones --------------
@@ -282,20 +328,21 @@ def weight_grad_x6(grad: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
 # same output -- a persistent kernel on one or two row tiles would run latency-bound (the masked
 # fp32-MFMA kernels took 120-128 us on a 224-row tail, profiles/r03r_*).
 
-def linear_tanh_mixed(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+def linear_tanh_mixed(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, planes: torch.Tensor | None = None) -> torch.Tensor:
     rows, k = x.shape
     n = w.shape[0]
     main = rows // 256 * 256
     if main == 0 or not x6_ok(main, k, n):
         return linear_tanh(x, w, b)
     y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
-    linear_tanh_x6(x[:main], w, b, out=y[:main])
+    linear_tanh_x6(x[:main], w, b, out=y[:main], planes=planes)
     if main < rows:
         torch.addmm(b, x[main:], w.t(), out=y[main:]).tanh_()
     return y
 
 
-def linear_tanh_out_mixed(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out: torch.Tensor, b_out: torch.Tensor):
+def linear_tanh_out_mixed(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out: torch.Tensor, b_out: torch.Tensor,
+                          planes: torch.Tensor | None = None):
     rows, k = x.shape
     n, k_out = w.shape[0], w_out.shape[0]
     main = rows // 256 * 256
@@ -303,35 +350,40 @@ def linear_tanh_out_mixed(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_o
         y = linear_tanh(x, w, b)
         return y, torch.addmm(b_out, y, w_out.t())
     y = torch.empty((rows, n), device=x.device, dtype=torch.float32)
-    _, o_main = linear_tanh_out_x6(x[:main], w, b, w_out, b_out, out=y[:main])
+    _, o_main = linear_tanh_out_x6(x[:main], w, b, w_out, b_out, out=y[:main], planes=planes)
     if main == rows:
         return y, o_main
     y_t = torch.addmm(b, x[main:], w.t(), out=y[main:]).tanh_()
     return y, torch.cat([o_main, torch.addmm(b_out, y_t, w_out.t())])
 
 
-def linear_tanh_backward_mixed(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.Tensor):
+def linear_tanh_backward_mixed(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.Tensor,
+                               out_db: torch.Tensor | None = None, planes: torch.Tensor | None = None):
+    """out_db: where to reduce the bias gradient into (the same tensor returned); planes: w_next's
+    weight_planes() with transpose True (None: split in the call)."""
     rows, k_next = gz_next.shape
     n = y.shape[1]
     main = rows // 256 * 256
     if main == 0 or not x6_ok(main, k_next, n):
-        return linear_tanh_backward(gz_next, w_next, y)
+        gz, db = linear_tanh_backward(gz_next, w_next, y)
+        return gz, (db if out_db is None else out_db.copy_(db))
     gz = torch.empty((rows, n), device=y.device, dtype=torch.float32)
-    _, db = linear_tanh_backward_x6(gz_next[:main], w_next, y[:main], out=gz[:main])
+    _, db = linear_tanh_backward_x6(gz_next[:main], w_next, y[:main], out=gz[:main], out_db=out_db, planes=planes)
     if main < rows:
         y_t = y[main:]
         gz_t = torch.mm(gz_next[main:], w_next, out=gz[main:]).mul_(1.0 - y_t * y_t)
-        db = db + gz_t.sum(0)
+        db = db.add_(gz_t.sum(0)) if out_db is not None else db + gz_t.sum(0)
     return gz, db
 
 
-def weight_grad_mixed(grad: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+def weight_grad_mixed(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """out: where to reduce the weight gradient into (the same tensor returned)."""
     rows, n_out = grad.shape
     k_in = x.shape[1]
     main = rows // 64 * 64
     if main == 0 or not x6_wgrad_ok(main, n_out, k_in):
-        return grad.t().mm(x)
-    dw = weight_grad_x6(grad[:main], x[:main])
+        return torch.mm(grad.t(), x, out=out)
+    dw = weight_grad_x6(grad[:main], x[:main], out=out)
     if main < rows:
         dw = dw.addmm_(grad[main:].t(), x[main:])
     return dw

@@ -243,3 +243,48 @@ def test_mixed_rows_match_fp64_gpu(rows):
     torch.testing.assert_close(dbm.double(), refb.sum(0), rtol=1e-5, atol=1e-5 * float(refb.sum(0).abs().max()))
     refw = g256.double().t() @ x.double()
     assert _rel(weight_grad_mixed(g256, x), refw)[0] < 4e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k", [(512, 256), (512, 512), (256, 512), (384, 128)])
+def test_weight_planes_feed_the_gemms_bit_exact_gpu(n, k):
+    """vss_weight_planes_bf16x6 (several weights' planes in one launch, the backward's W^T read straight
+    from the (k_next, n) weight): the GEMM entries given those planes and a NULL weight produce the same
+    bits as when they split (and, for the backward, transpose) the weight themselves."""
+    from vss_amd.update import linear_tanh_out_x6, weight_planes
+    g = torch.Generator(device="cuda").manual_seed(n + k)
+    rows = 2048
+    w = torch.randn(n, k, device="cuda", generator=g) / k ** 0.5
+    b = torch.randn(n, device="cuda", generator=g) * 0.1
+    x = torch.tanh(torch.randn(rows, k, device="cuda", generator=g))
+    w_next = torch.randn(k, n, device="cuda", generator=g) / n ** 0.5  # backward: (k_next, n) weight
+    gz = torch.randn(rows, k, device="cuda", generator=g) * 1e-3
+    y = torch.tanh(torch.randn(rows, n, device="cuda", generator=g))
+    pf, pb, pf2 = weight_planes([(w, False), (w_next, True), (w, False)])
+    assert torch.equal(pf, pf2)
+    assert torch.equal(linear_tanh_x6(x, w, b, planes=pf), linear_tanh_x6(x, w, b))
+    g1, d1 = linear_tanh_backward_x6(gz, w_next, y, planes=pb)
+    g2, d2 = linear_tanh_backward_x6(gz, w_next, y)
+    assert torch.equal(g1, g2) and torch.equal(d1, d2)
+    if n == 256:
+        wo, bo = torch.randn(2, 256, device="cuda", generator=g), torch.zeros(2, device="cuda")
+        y1, o1 = linear_tanh_out_x6(x, w, b, wo, bo, planes=pf)
+        y2, o2 = linear_tanh_out_x6(x, w, b, wo, bo)
+        assert torch.equal(y1, y2) and torch.equal(o1, o2)
+
+
+@pytest.mark.gpu
+def test_weight_planes_refusals_gpu():
+    from vss_amd.update import weight_planes
+    w = torch.randn(256, 512, device="cuda")
+    with pytest.raises(ValueError):
+        weight_planes([])
+    with pytest.raises(ValueError):
+        weight_planes([(w, False)] * 9)
+    with pytest.raises(N.NativeError):
+        weight_planes([(torch.randn(100, 512, device="cuda"), False)])  # n % 128
+    with pytest.raises(N.NativeError):
+        weight_planes([(torch.randn(256, 100, device="cuda"), False)])  # k % 64
+    with pytest.raises(ValueError):
+        linear_tanh_x6(torch.randn(256, 512, device="cuda"), w, torch.zeros(256, device="cuda"),
+                       planes=torch.empty(3, 10, device="cuda", dtype=torch.int16))

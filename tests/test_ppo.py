@@ -76,6 +76,35 @@ def test_flat_grads_are_views():
         off += p.numel()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,act_dim", [(131_072, 2), (4096, 6), (65_728, 2)])
+def test_zeroed_backward_writes_the_autograd_gradients_gpu(rows, act_dim):
+    """FlatGrads.zeroed_backward: the MLPs' backward (_TanhMLP) reduces its gradients straight into the
+    FlatGrads views instead of handing them to autograd's accumulation.  Same values as the plain
+    autograd gradients of the same loss (torch.autograd.grad, which takes the accumulation path and
+    leaves .grad alone), every parameter, bit for bit; the buffer's previous contents do not leak in."""
+    torch.manual_seed(act_dim)
+    agent = make_agent(act_dim).cuda()
+    flat = P.FlatGrads(agent)
+    g = torch.Generator(device="cuda").manual_seed(rows)
+    obs = torch.randn(rows, 52, device="cuda", generator=g)
+    act = torch.randn(rows, act_dim, device="cuda", generator=g) * 0.5
+    n = rows - 64  # padding rows beyond the minibatch, as the update pads it
+    logp, adv, ret, val = (torch.randn(n, device="cuda", generator=g) for _ in range(4))
+    args = _args()
+
+    def losses():
+        return P.minibatch_losses(agent, args, obs, act, logp - 3.0, adv, ret, val)[0]
+
+    want = torch.autograd.grad(losses(), list(agent.parameters()))
+    assert float(flat.flat.abs().sum()) == 0.0  # torch.autograd.grad left .grad alone
+    flat.flat.fill_(7.0)  # stale contents: zeroed_backward must zero them first
+    flat.zeroed_backward(losses())
+    for (name, p), w in zip(agent.named_parameters(), want):
+        assert torch.equal(p.grad, w), name
+    assert not P._DIRECT_GRADS[0]
+
+
 def _args(**kw):
     a = P.parse_args([])
     a.update_epochs, a.num_minibatches = 2, 2

@@ -10,6 +10,9 @@ tools/gemm_x6_variants.py:
   notanh    the forward epilogue adds the bias but skips the tanh (its VALU cost)
   noy       the backward epilogue reuses the prefetched first y row group for every row group
             (the cost of the epilogue's y loads)
+  noepi     the forward / backward epilogues neither transform nor store (a never-true guard keeps
+            the accumulators live): the K loop's time alone
+  nobar     the K loop's two barriers per K-tile pair removed (races: timing only)
 Earlier ablations (nobar, nopstage, wab; profiles/r03k_*, r03p_*) ran on earlier versions of the
 kernel and were retired with the code they patched.
 Usage: python tools/x6_ablate.py nosplit noglobal nosplit+noglobal"""
@@ -31,6 +34,15 @@ PATCH = {
     "notanh": [("v[r] = tanh_f32(v[r] + epi_lds[il + r]);", "v[r] = v[r] + epi_lds[il + r];")],
     "noy": [("yrest[j][i] = *reinterpret_cast<const f32x4*>(a.y + ((int64_t)jb + 16 * j + fr) * a.ldo + ib + 16 * i + 4 * fg);",
              "yrest[j][i] = ypre[0][i];")],
+    "noepi": [("          for (int r = 0; r < 4; ++r) v[r] = tanh_f32(v[r] + epi_lds[il + r]);\n          *reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig) = v;",
+               "          for (int r = 0; r < 1; ++r) (void)r;\n          if (v[0] == 1234.5f) *reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig) = v;"),
+              ("          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig));",
+               "          if (v[0] == 1234.5f) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig));"),
+              ("            v[r] = v[r] * fmaf(-yv[r], yv[r], 1.0f);\n            cs[i][r] += v[r];", "            (void)yv;"),
+              ("yrest[j][i] = *reinterpret_cast<const f32x4*>(a.y + ((int64_t)jb + 16 * j + fr) * a.ldo + ib + 16 * i + 4 * fg);",
+               "yrest[j][i] = ypre[0][i];")],
+    "nobar": [("      swrite(r1, 1);\n      __syncthreads();", "      swrite(r1, 1);"),
+              ("      swrite(r0, 0);\n      __syncthreads();", "      swrite(r0, 0);")],
     # the K loop issues no global loads (the staged registers are written again as they are)
     "noglobal": [("      gload(r1);\n", ""), ("      gload(r0);\n", "")],
 }

@@ -13,6 +13,12 @@ tools/gemm_x6_variants.py:
   noepi     the forward / backward epilogues neither transform nor store (a never-true guard keeps
             the accumulators live): the K loop's time alone
   nobar     the K loop's two barriers per K-tile pair removed (races: timing only)
+  iouter    (correct results) the k-step's MFMAs i-tile-outer: the Q fragments held, the P fragments of
+            one i tile at a time (72 instead of 96 fragment registers)
+  ypreN     (correct results) the backward requests N of its 4 y row groups during the item's last
+            K-tile pair (1 in the product)
+  staggerN  (correct results) the forward / backward blocks of a row band start in N phases spread over
+            one item, so that their epilogues' HBM traffic does not arrive all at once
 Earlier ablations (nobar, nopstage, wab; profiles/r03k_*, r03p_*) ran on earlier versions of the
 kernel and were retired with the code they patched.
 Usage: python tools/x6_ablate.py nosplit noglobal nosplit+noglobal"""
@@ -43,6 +49,12 @@ PATCH = {
                "yrest[j][i] = ypre[0][i];")],
     "nobar": [("      swrite(r1, 1);\n      __syncthreads();", "      swrite(r1, 1);"),
               ("      swrite(r0, 0);\n      __syncthreads();", "      swrite(r0, 0);")],
+    "stagger2": [("constexpr int kStagger = 0;", "constexpr int kStagger = 2;")],
+    "stagger4": [("constexpr int kStagger = 0;", "constexpr int kStagger = 4;")],
+    "stagger8": [("constexpr int kStagger = 0;", "constexpr int kStagger = 8;")],
+    "iouter": [('    u32x4 pf[3][TI], qf[3][TJ];\n    const char* pk = lds + buf * C::BUF;                    // ST_KROW images: plane 0 of P\n    const char* qk = lds + buf * C::BUF + Img<BI>::BYTES;  // and of Q\n#pragma unroll\n    for (int pl = 0; pl < 3; ++pl) {\n#pragma unroll\n      for (int i = 0; i < TI; ++i) {\n        if constexpr (SP == ST_KROW) {\n          const int i0 = wi * C::WTI + 16 * i;\n          pf[pl][i] = tr_frag(pk + pl * KImg<BI>::PS + kfrag_off(i0, lane, 0), pk + pl * KImg<BI>::PS + kfrag_off(i0, lane, 1));\n        } else {\n          pf[pl][i] = *reinterpret_cast<const u32x4*>(pb + pl * Img<BI>::PS + i * 256);\n        }\n      }\n#pragma unroll\n      for (int j = 0; j < TJ; ++j) {\n        if constexpr (SQ == ST_KROW) {\n          const int j0 = wj * C::WTJ + 16 * j;\n          qf[pl][j] = tr_frag(qk + pl * KImg<BJ>::PS + kfrag_off(j0, lane, 0), qk + pl * KImg<BJ>::PS + kfrag_off(j0, lane, 1));\n        } else {\n          qf[pl][j] = *reinterpret_cast<const u32x4*>(qb + pl * Img<BJ>::PS + j * 256);\n        }\n      }\n    }\n    if constexpr (PDMA) {\n      __builtin_amdgcn_sched_barrier(0);\n      between();\n      __builtin_amdgcn_sched_barrier(0);\n    }\n    // the six products, smallest first: lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi\n    constexpr int PP[6] = {2, 0, 1, 1, 0, 0};\n    constexpr int QP[6] = {0, 2, 1, 0, 1, 0};\n#pragma unroll\n    for (int x = 0; x < 6; ++x)\n#pragma unroll\n      for (int i = 0; i < TI; ++i)\n#pragma unroll\n        for (int j = 0; j < TJ; ++j)\n          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pf[PP[x]][i]),\n                                                              __builtin_bit_cast(bf16x8, qf[QP[x]][j]), acc[i][j], 0, 0, 0);\n', '    u32x4 qf[3][TJ];\n    const char* pk = lds + buf * C::BUF;                    // ST_KROW images: plane 0 of P\n    const char* qk = lds + buf * C::BUF + Img<BI>::BYTES;  // and of Q\n    auto read_p = [&](int pl, int i) -> u32x4 {\n      if constexpr (SP == ST_KROW) {\n        const int i0 = wi * C::WTI + 16 * i;\n        return tr_frag(pk + pl * KImg<BI>::PS + kfrag_off(i0, lane, 0), pk + pl * KImg<BI>::PS + kfrag_off(i0, lane, 1));\n      } else {\n        return *reinterpret_cast<const u32x4*>(pb + pl * Img<BI>::PS + i * 256);\n      }\n    };\n#pragma unroll\n    for (int pl = 0; pl < 3; ++pl) {\n#pragma unroll\n      for (int j = 0; j < TJ; ++j) {\n        if constexpr (SQ == ST_KROW) {\n          const int j0 = wj * C::WTJ + 16 * j;\n          qf[pl][j] = tr_frag(qk + pl * KImg<BJ>::PS + kfrag_off(j0, lane, 0), qk + pl * KImg<BJ>::PS + kfrag_off(j0, lane, 1));\n        } else {\n          qf[pl][j] = *reinterpret_cast<const u32x4*>(qb + pl * Img<BJ>::PS + j * 256);\n        }\n      }\n    }\n    u32x4 pc[3], pn[3];\n#pragma unroll\n    for (int pl = 0; pl < 3; ++pl) pc[pl] = read_p(pl, 0);\n    // the six products, smallest first: lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi (per accumulator\n    // the same order as product-outer: the same bits)\n    constexpr int PP[6] = {2, 0, 1, 1, 0, 0};\n    constexpr int QP[6] = {0, 2, 1, 0, 1, 0};\n#pragma unroll\n    for (int i = 0; i < TI; ++i) {\n      if (i + 1 < TI) {\n#pragma unroll\n        for (int pl = 0; pl < 3; ++pl) pn[pl] = read_p(pl, i + 1);\n      }\n      if constexpr (PDMA) {\n        if (i == TI - 1) {\n          __builtin_amdgcn_sched_barrier(0);\n          between();\n          __builtin_amdgcn_sched_barrier(0);\n        }\n      }\n#pragma unroll\n      for (int x = 0; x < 6; ++x)\n#pragma unroll\n        for (int j = 0; j < TJ; ++j)\n          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pc[PP[x]]),\n                                                              __builtin_bit_cast(bf16x8, qf[QP[x]][j]), acc[i][j], 0, 0, 0);\n#pragma unroll\n      for (int pl = 0; pl < 3; ++pl) pc[pl] = pn[pl];\n    }\n')],
+    "ypre2": [("constexpr int kYPre = 1;", "constexpr int kYPre = 2;")],
+    "ypre4": [("constexpr int kYPre = 1;", "constexpr int kYPre = 4;")],
     # the K loop issues no global loads (the staged registers are written again as they are)
     "noglobal": [("      gload(r1);\n", ""), ("      gload(r0);\n", "")],
 }

@@ -15,6 +15,8 @@ tools/gemm_x6_variants.py:
   biasinit  (correct results, other rounding) the forward's accumulators start at the bias instead of
             zero (no bias add in the epilogue)
   fasttanh  (less accurate: timing only) tanh as 2 / (1 + exp(-2z)) - 1
+  stcontig  (timing only) every epilogue store instruction writes 1 KB of contiguous memory
+  ldcontig  (timing only) every backward epilogue y load (but the prefetched group) reads 1 KB contiguous
   nostore   the forward / backward epilogues compute everything but store only under a never-true guard
   nobar     the K loop's two barriers per K-tile pair removed (races: timing only)
   iouter    (correct results) the k-step's MFMAs i-tile-outer: the Q fragments held, the P fragments of
@@ -74,6 +76,14 @@ PATCH = {
                  ("for (int r = 0; r < 4; ++r) v[r] = tanh_f32(v[r] + epi_lds[il + r]);", "for (int r = 0; r < 4; ++r) v[r] = tanh_f32(v[r]);")],
     "fasttanh": [("for (int r = 0; r < 4; ++r) v[r] = tanh_f32(v[r] + epi_lds[il + r]);",
                   "for (int r = 0; r < 4; ++r) v[r] = fmaf(2.0f, __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.8853900817779268f * (v[r] + epi_lds[il + r]))), -1.0f);")],
+    # timing only: each epilogue store / y load instruction on 1 KB of contiguous memory (the same bytes
+    # per item, other addresses) instead of 16 rows x 64 B
+    "stcontig": [("          *reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig) = v;",
+                  "          *reinterpret_cast<f32x4*>(a.out + (((int64_t)(it * a.nj + jt) * (C::THREADS / 64) + wv) * (TI * TJ) + i * TJ + j) * 256 + lane * 4) = v;"),
+                 ("          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig));",
+                  "          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(a.out + (((int64_t)(it * a.nj + jt) * (C::THREADS / 64) + wv) * (TI * TJ) + i * TJ + j) * 256 + lane * 4));")],
+    "ldcontig": [("yrest[j][i] = *reinterpret_cast<const f32x4*>(a.y + ((int64_t)jb + 16 * j + fr) * a.ldo + ib + 16 * i + 4 * fg);",
+                  "yrest[j][i] = *reinterpret_cast<const f32x4*>(a.y + (((int64_t)(it * a.nj + jt) * (C::THREADS / 64) + wv) * (TI * TJ) + i * TJ + j) * 256 + lane * 4);")],
     # the K loop issues no global loads (the staged registers are written again as they are)
     "noglobal": [("      gload(r1);\n", ""), ("      gload(r0);\n", "")],
 }

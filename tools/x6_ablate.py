@@ -15,6 +15,9 @@ tools/gemm_x6_variants.py:
   biasinit  (correct results, other rounding) the forward's accumulators start at the bias instead of
             zero (no bias add in the epilogue)
   fasttanh  (less accurate: timing only) tanh as 2 / (1 + exp(-2z)) - 1
+  onewave   (correct results) the forward / backward's 256 x 128 block as 4 waves of 64 x 128 (one wave per
+            SIMD, 512 registers) instead of 8 of 64 x 64
+  fwdnt     (correct results) the forward's epilogue stores nontemporal, as the backward's
   stcontig  (timing only) every epilogue store instruction writes 1 KB of contiguous memory
   ldcontig  (timing only) every backward epilogue y load (but the prefetched group) reads 1 KB contiguous
   nostore   the forward / backward epilogues compute everything but store only under a never-true guard
@@ -84,6 +87,9 @@ PATCH = {
                   "          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(a.out + (((int64_t)(it * a.nj + jt) * (C::THREADS / 64) + wv) * (TI * TJ) + i * TJ + j) * 256 + lane * 4));")],
     "ldcontig": [("yrest[j][i] = *reinterpret_cast<const f32x4*>(a.y + ((int64_t)jb + 16 * j + fr) * a.ldo + ib + 16 * i + 4 * fg);",
                   "yrest[j][i] = *reinterpret_cast<const f32x4*>(a.y + (((int64_t)(it * a.nj + jt) * (C::THREADS / 64) + wv) * (TI * TJ) + i * TJ + j) * 256 + lane * 4);")],
+    "fwdnt": [("          *reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig) = v;",
+               "          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig));")],
+    "onewave": [("using CfgB = Cfg<256, 128, 4, 2>;", "using CfgB = Cfg<256, 128, 4, 1>;")],
     # the K loop issues no global loads (the staged registers are written again as they are)
     "noglobal": [("      gload(r1);\n", ""), ("      gload(r0);\n", "")],
 }

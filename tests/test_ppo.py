@@ -340,6 +340,28 @@ def test_train_end_to_end_gpu(env_id, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("env_id", ["sa", "dma"])
+def test_train_is_bit_reproducible_gpu(env_id, tmp_path):
+    """The whole loop -- env steps (Philox per field), the rollout policy and its sampling, GAE, the
+    captured update minibatches (their replay-12 self-check included), Adam -- run twice with the same
+    seed in one process gives the same parameters and the same logged losses, bit for bit: every
+    reduction on the path has a fixed order (no float atomics)."""
+    def run(sub):
+        args = P.parse_args(["--env-id", env_id, "--num-envs", "4095",
+                             "--num-steps", "16", "--num-updates", "3", "--seed", "5",
+                             "--save-path", str(tmp_path / sub)])
+        agent, hist = P.train(args)
+        return [p.detach().clone() for p in agent.parameters()], hist
+
+    p1, h1 = run("a")
+    p2, h2 = run("b")
+    assert all(torch.equal(a, b) for a, b in zip(p1, p2))
+    for r1, r2 in zip(h1, h2):
+        for k in ("v_loss", "pg_loss", "entropy", "approx_kl"):
+            assert r1[k] == r2[k], (k, r1[k], r2[k])
+
+
+@pytest.mark.gpu
 def test_train_sa_65536_envs_config3(tmp_path):
     """BASELINE config 3: the full SA train loop at 65,536 envs with the reference's update
     defaults (T = 128, 8 epochs x 4 minibatches, fp32), one update: finite losses, the timing

@@ -19,6 +19,8 @@ tensors (the CPU test suite's PPO loop) take the same formulas in torch.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _native as N
@@ -212,7 +214,6 @@ def weight_planes(jobs) -> list:
     valid until the weights change."""
     if not 1 <= len(jobs) <= 8:
         raise ValueError(f"weight_planes: 1..8 weights per launch, got {len(jobs)}")
-    import ctypes
     ws, ns, ks, ts, outs = [], [], [], [], []
     for w, tr in jobs:
         if w.dim() != 2 or w.dtype != torch.float32 or not w.is_cuda or not w.is_contiguous():

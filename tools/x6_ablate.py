@@ -30,7 +30,7 @@ tools/gemm_x6_variants.py:
   that their epilogues do not reach HBM at once, changed nothing and was not kept:
   profiles/r04_gemm_x6_stagger_iouter_not_kept.log; nor did a ring of four register-staged K tiles in
   flight instead of two, profiles/r04_gemm_x6_depth4_ring_not_kept.log)
-Earlier ablations (nobar, nopstage, wab; profiles/r03k_*, r03p_*) ran on earlier versions of the
+Earlier ablations (nopstage, wab; profiles/r03k_*, r03p_*) ran on earlier versions of the
 kernel and were retired with the code they patched.
 Usage: python tools/x6_ablate.py nosplit noglobal nosplit+noglobal"""
 import os

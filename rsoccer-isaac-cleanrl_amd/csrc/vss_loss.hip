@@ -68,17 +68,17 @@ __global__ __launch_bounds__(kThreads) void loss_rows_kernel(int64_t rows, int64
   for (int k = 0; k < K; ++k) acc[k] = 0.f;
   const int64_t stride = (int64_t)gridDim.x * kThreads;
   for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < rows_pad; r += stride) {
+    if (r >= rows) {  // padding rows: no loss term, no gradient (and no input read)
+#pragma unroll
+      for (int a = 0; a < NA; ++a) g_mean[r * NA + a] = 0.f;
+      g_value[r] = 0.f;
+      continue;
+    }
     float mu[NA], x[NA];
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
       mu[a] = mean[r * NA + a];
       x[a] = action[r * NA + a];
-    }
-    if (r >= rows) {  // padding rows: no loss term, no gradient
-#pragma unroll
-      for (int a = 0; a < NA; ++a) g_mean[r * NA + a] = 0.f;
-      g_value[r] = 0.f;
-      continue;
     }
     float nlp = 0.f;
     float dz[NA];

@@ -58,7 +58,7 @@ from envs._gym import Box, ObservationWrapper  # noqa: E402
 from vss_amd.loss import ppo_loss  # noqa: E402
 from vss_amd.update import (gemm_shape_ok, linear_tanh, linear_tanh_backward, linear_tanh_backward_mixed,  # noqa: E402
                             linear_tanh_mixed, linear_tanh_out, linear_tanh_out_mixed, linear_tanh_out_ok,
-                            output_backward, output_backward_ok, tanh_grad_bias, weight_grad_mixed, weight_planes,
+                            output_backward, output_backward_ok, weight_grad_mixed, weight_planes,
                             x6_ok)
 
 
@@ -168,28 +168,12 @@ class Agent(nn.Module):
         return action, probs.log_prob(action).sum(1), probs.entropy().sum(1), self.critic(x)
 
 
-# ---- the update's Linear layers with a split-K weight gradient ------------------------------------
-# dW = dY^T X reduces over all minibatch rows (2,097,152 at 65,536 envs) into a small output
-# (<= 512 x 512); as one GEMM hipBLASLt runs the 256<->512, first and last layers of the Agent at
-# 0.6-72 TF.  Splitting the rows into SPLITK chunks (one batched GEMM + a sum) runs them at
-# ~150 TF (tools/wgrad_bench.py): -0.9 s per update.  Forward and input gradient are unchanged
-# (addmm with bias = what nn.Linear issues; dY W); only the fp32 summation order of dW differs.
+# ---- the update's MLPs ---------------------------------------------------------------------------------
+# The first layer's weight gradient dW = dY^T X reduces over all minibatch rows (2,097,152 at 65,536 envs)
+# into a (256, 52) output; as one GEMM hipBLASLt runs it at ~1 TF.  Splitting the rows into SPLITK chunks
+# (one batched GEMM + a sum) runs it at ~90 TF (tools/wgrad_bench.py); only the fp32 summation order differs.
 SPLITK = 64
 SPLITK_MIN_ROWS = 32768
-TANH_GRAD_COLS = (64, 128, 256, 512, 1024)  # widths vss_tanh_grad_bias takes (the Agent's: 256, 512)
-
-
-class _LinearSplitK(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, weight, bias):
-        ctx.save_for_backward(x, weight)
-        return torch.addmm(bias, x, weight.t())
-
-    @staticmethod
-    def backward(ctx, gy):
-        x, weight = ctx.saved_tensors
-        gx = gy.mm(weight) if ctx.needs_input_grad[0] else None
-        return gx, _split_k_wgrad(gy, x), gy.sum(0)
 
 
 def _split_k_wgrad(gz, x, out=None):
@@ -201,26 +185,6 @@ def _split_k_wgrad(gz, x, out=None):
                                  x[:main].reshape(SPLITK, main // SPLITK, x.shape[1])), 0, out=out)
         return dw.addmm_(gz[main:].t(), x[main:]) if main < rows else dw
     return torch.mm(gz.t(), x, out=out)
-
-
-class _LinearTanh(torch.autograd.Function):
-    """nn.Linear followed by nn.Tanh (the Agent's hidden layers, ppo…:104-111): the same forward
-    (addmm with bias, then tanh, here in place on the addmm output); the backward takes
-    gz = gy * (1 - y^2) and the bias gradient in ONE pass (vss_tanh_grad_bias, HIP) instead of
-    torch's tanh_backward + a separate reduction, then dX and split-K dW as _LinearSplitK."""
-
-    @staticmethod
-    def forward(ctx, x, weight, bias):
-        y = torch.addmm(bias, x, weight.t()).tanh_()
-        ctx.save_for_backward(x, weight, y)
-        return y
-
-    @staticmethod
-    def backward(ctx, gy):
-        x, weight, y = ctx.saved_tensors
-        gz, gb = tanh_grad_bias(gy, y)
-        gx = gz.mm(weight) if ctx.needs_input_grad[0] else None
-        return gx, _split_k_wgrad(gz, x), gb
 
 
 class _TanhMLP(torch.autograd.Function):
@@ -242,18 +206,18 @@ class _TanhMLP(torch.autograd.Function):
         rows = x.shape[0]
         x6 = x.is_cuda and UPDATE_GEMM == "x6"
         # the x6 layers' weight planes, forward (W) and backward (W^T), in one launch for the whole MLP
-        pf, ctx.planes_b = _mlp_planes(ws, rows) if x6 and WEIGHT_PLANES else ({}, {})
+        pf, ctx.planes_b = _mlp_planes(ws, rows) if x6 else ({}, {})
         for layer, (w, b) in enumerate(zip(ws[:-2], bs[:-2])):
             if x6:
                 hs.append(linear_tanh_mixed(hs[-1], w, b, planes=pf.get(layer)))
             else:
                 hs.append(linear_tanh(hs[-1], w, b))
-        if x6 and OUTPUT_FWD:
+        if x6:
             # the last hidden layer and the output layer in one launch per row range (the whole 256-row
             # tiles through vss_linear_tanh_out_bf16x6, the rest through vss_linear_tanh + addmm)
             h, out = linear_tanh_out_mixed(hs[-1], ws[-2], bs[-2], ws[-1], bs[-1], planes=pf.get(len(ws) - 2))
             hs.append(h)
-        elif x.is_cuda and OUTPUT_FWD and linear_tanh_out_ok(rows, ws[-2].shape[1], ws[-2].shape[0], ws[-1].shape[0]):
+        elif x.is_cuda and linear_tanh_out_ok(rows, ws[-2].shape[1], ws[-2].shape[0], ws[-1].shape[0]):
             # the last hidden layer and the output layer in one launch (vss_linear_tanh_out)
             h, out = linear_tanh_out(hs[-1], ws[-2], bs[-2], ws[-1], bs[-1])
             hs.append(h)
@@ -273,7 +237,7 @@ class _TanhMLP(torch.autograd.Function):
         gz = gout.contiguous()  # pre-activation gradient of the current layer
         gb = torch.sum(gz, 0, out=dst[2 * n - 1])
         for layer in reversed(range(n)):
-            if OUTPUT_BWD and layer == n - 1 and layer > 0 and output_backward_ok(gz.shape[1], hs[layer].shape[1]):
+            if layer == n - 1 and layer > 0 and output_backward_ok(gz.shape[1], hs[layer].shape[1]):
                 # the output layer (1-6 columns): its weight gradient and the backward into the tanh
                 # layer below in one streaming pass over that layer's output (vss_output_backward)
                 grads[2 * layer + 1] = gb
@@ -329,25 +293,12 @@ def _mlp_planes(ws, rows: int):
     return pf, pb
 
 
-# the x6 weights' planes: "1" (default) = one vss_weight_planes_bf16x6 launch per MLP and minibatch
-# (forward W and backward W^T), "0" = each GEMM entry splits (and the backward transposes) its weight
-WEIGHT_PLANES = os.environ.get("VSS_WEIGHT_PLANES", "1") == "1"
-
-# the update's MLP path: "fused" (default) = _TanhMLP (our fp32 MFMA GEMMs with the tanh work in
-# their epilogues: 3.51 s per SA update at 65,536 envs); "split" = _LinearTanh / _LinearSplitK
-# (hipBLASLt GEMMs + the one-pass HIP tanh backward: 3.99 s).  DESIGN.md §5.3 / §7,
-# profiles/r02_gemm_fused_bench.log, profiles/r02_ppo_sa_fused_vs_split_seeds.json.
-UPDATE_MLP = os.environ.get("VSS_UPDATE_MLP", "fused")
 # the fused path's GEMM arithmetic: "x6" (default) = fp32 products on the bf16 matrix cores from an
 # exact 3-way bf16 split of every operand (csrc/vss_gemm_x6.hip; error vs fp64 at or below the fp32
-# GEMMs', tests/test_gemm_x6.py), where the shapes are exact; "fp32" = the fp32-MFMA kernels only
+# GEMMs', tests/test_gemm_x6.py), where the shapes are exact; "fp32" = the fp32-MFMA kernels only.
+# (The round-4 A/B switches VSS_UPDATE_MLP=split, VSS_OUTPUT_FWD/BWD=0 and VSS_WEIGHT_PLANES=0, each
+# strictly slower, are retired from the product: tools/ab_switches_r04.patch re-adds them for A/B runs.)
 UPDATE_GEMM = os.environ.get("VSS_UPDATE_GEMM", "x6")
-# the fused path's output layer: "1" (default) = its backward and weight gradient in one streaming
-# pass (vss_output_backward), "0" = the padded backward + a split-K dW GEMM (A/B switch)
-OUTPUT_BWD = os.environ.get("VSS_OUTPUT_BWD", "1") == "1"
-# ... and its forward: "1" (default) = folded into the last hidden layer's GEMM epilogue
-# (vss_linear_tanh_out) where the shapes allow, "0" = a separate addmm (A/B switch)
-OUTPUT_FWD = os.environ.get("VSS_OUTPUT_FWD", "1") == "1"
 
 
 def _fused_mlp_ok(seq: nn.Sequential) -> bool:
@@ -363,32 +314,18 @@ def _fused_mlp_ok(seq: nn.Sequential) -> bool:
 
 
 def _mlp_forward(seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
-    if UPDATE_MLP == "fused" and x.dtype == torch.float32 and _fused_mlp_ok(seq):
+    """The update's MLP: _TanhMLP for the Agent's (Linear, Tanh) x L + Linear stacks in fp32, the module
+    itself (torch autograd) for anything else."""
+    if x.dtype == torch.float32 and _fused_mlp_ok(seq):
         params = [t for m in list(seq)[0::2] for t in (m.weight, m.bias)]
         return _TanhMLP.apply(x, *params)
-    mods = list(seq)
-    i = 0
-    while i < len(mods):
-        m = mods[i]
-        if isinstance(m, nn.Linear) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.Tanh) \
-                and m.out_features in TANH_GRAD_COLS:
-            x = _LinearTanh.apply(x, m.weight, m.bias)
-            i += 2
-            continue
-        if isinstance(m, nn.Linear):
-            x = _LinearSplitK.apply(x, m.weight, m.bias)
-        elif isinstance(m, nn.Tanh):
-            x = torch.tanh(x)
-        else:
-            x = m(x)
-        i += 1
-    return x
+    return seq(x)
 
 
 def get_action_and_value_update(agent: "Agent", x, action):
     """Agent.get_action_and_value (ppo…:157-164) on the same parameters, for the PPO update: the
     same function (forward within fp32 rounding: fused GEMM summation order and a few-ulp tanh),
-    the MLPs through _TanhMLP, split-K weight gradients in the backward."""
+    the MLPs through _TanhMLP."""
     mean = _mlp_forward(agent.actor_mean, x)
     std = torch.exp(agent.actor_logstd.expand_as(mean))
     # no argument validation: its finiteness check is a host sync per minibatch, which a captured
@@ -613,9 +550,20 @@ def value_loss(newvalue, mb_returns, mb_values, clip_coef: float, clip_vloss: bo
 # hidden-layer GEMM runs on whole x6 tiles: at 4,095 envs a 131,040-row minibatch otherwise leaves
 # 224-row tails that hipBLASLt runs on one or two workgroups (43-110 us each, ~21 ms per update)
 MLP_ROW_PAD = 256
-# MinibatchGraph re-runs this replay eagerly and compares the two bit for bit (once per training run;
-# round 3's packet-capture failure began at the 9th replay, profiles/r03w_graph_probe2.log)
+# MinibatchGraph re-runs replays 12, 48, 192, ... (GRAPH_CHECK_REPLAY x GRAPH_CHECK_FACTOR^m) eagerly and
+# compares each with its replay bit for bit: round 3's packet-capture failure began at the 9th replay
+# (profiles/r03w_graph_probe2.log), and a later onset is caught at the next check; the checks cost one eager
+# minibatch each, O(log replays) per run
 GRAPH_CHECK_REPLAY = 12
+GRAPH_CHECK_FACTOR = 4
+
+
+def graph_check_due(replays: int) -> bool:
+    """Whether replay number `replays` (1-based) of a MinibatchGraph is re-run eagerly and compared."""
+    r = GRAPH_CHECK_REPLAY
+    while r < replays:
+        r *= GRAPH_CHECK_FACTOR
+    return r == replays
 
 
 def minibatch_losses(agent, args, obs, actions, logprobs, adv, returns, values):
@@ -703,7 +651,7 @@ class MinibatchGraph:
             self._capture()
         self.graph.replay()
         self.replays += 1
-        if self.replays == GRAPH_CHECK_REPLAY:
+        if graph_check_due(self.replays):
             return self._check()
         return self.out
 
@@ -730,11 +678,25 @@ def padding_rows(mb: int, device) -> int:
     return (-mb) % MLP_ROW_PAD if torch.device(device).type == "cuda" else 0
 
 
+_WARNED_PACKET_CAPTURE = [False]
+
+
 def make_minibatch_graph(agent, flat, args, batch, obs_dim, act_dim, device):
-    """MinibatchGraph when --update-graph applies (ROCm GPU, fp32, equal minibatches), else None."""
+    """MinibatchGraph when --update-graph applies (ROCm GPU, fp32, equal minibatches, and the runtime
+    started with graph packet capture off), else None: the update then runs eagerly."""
     mb = batch // args.num_minibatches
     if not getattr(args, "update_graph", False) or torch.device(device).type != "cuda" or \
             getattr(args, "amp", "none") != "none" or batch % mb:
+        return None
+    if os.environ.get(_PACKET_CAPTURE) != "0":
+        # a caller that initialised the GPU before disable_graph_packet_capture() (or chose packet capture
+        # on): no capture -- round 3's corrupted replays ran in that mode (profiles/r03w_graph_probe2.log)
+        if not _WARNED_PACKET_CAPTURE[0]:
+            import warnings
+            warnings.warn(f"{_PACKET_CAPTURE}={os.environ.get(_PACKET_CAPTURE, '<unset>')}: the runtime started "
+                          "with graph packet capture on, so the update minibatches run eagerly (call "
+                          "disable_graph_packet_capture() before anything initialises the GPU)", RuntimeWarning)
+            _WARNED_PACKET_CAPTURE[0] = True
         return None
     return MinibatchGraph(agent, flat, args, mb, obs_dim, act_dim, device)
 
@@ -847,6 +809,7 @@ def train(args, on_update=None):
     """The PPO loop (ppo…:231-379).  on_update(record, agent) -- optional, called after every update
     with that update's history record -- may return True to stop training early (tools/time_to_score.py
     evaluates the live policy there)."""
+    disable_graph_packet_capture()  # effective only while nothing has initialised the GPU yet
     world, rank, local = setup_distributed()
     run_name = f"{args.exp_name}_ppo-{args.env_id}_{args.seed}"
     writer = make_writer(args, run_name, rank)

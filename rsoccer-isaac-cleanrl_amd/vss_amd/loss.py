@@ -101,6 +101,14 @@ def ppo_loss(mean, logstd, value, action, logprob_old, adv, returns, values_old,
     if not ppo_loss_ok(mean, value) or rows == 0:
         raise ValueError(f"vss_ppo_loss: fp32 ROCm tensors with n_act in {N_ACT} and rows > 0 required, "
                          f"got {mean.dtype} {tuple(mean.shape)}")
+    # the kernel reads every input as fp32 device memory: the action rows must cover the network rows
+    # (padding included), and nothing may be a CPU, fp64 or other-device tensor
+    if action.shape[0] < mean.shape[0]:
+        raise ValueError(f"vss_ppo_loss: action has {action.shape[0]} rows, fewer than the {mean.shape[0]} network rows")
+    for name, t in (("logstd", logstd), ("action", action), ("logprob_old", logprob_old), ("adv", adv),
+                    ("returns", returns), ("values_old", values_old)):
+        if t.dtype != torch.float32 or t.device != mean.device:
+            raise ValueError(f"vss_ppo_loss: {name} must be fp32 on {mean.device}, got {t.dtype} on {t.device}")
     loss, stats = _PPOLoss.apply(mean, logstd, value.reshape(-1, 1), action[:mean.shape[0]], logprob_old, adv, returns,
                                  values_old, clip_coef, ent_coef, vf_coef, clip_vloss)
     return loss, tuple(stats[i] for i in range(6))

@@ -58,6 +58,35 @@ def test_ppo_loss_refuses_bad_shapes_cpu():
 @pytest.mark.parametrize("clip_vloss", [False, True])
 @pytest.mark.parametrize("norm_adv", [True, False])
 def test_fused_loss_matches_reference_autograd_gpu(n_act, clip_vloss, norm_adv):
+    _check_fused_loss(n_act, clip_vloss, norm_adv)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_act", [1, 3, 4, 8])
+@pytest.mark.parametrize("clip_vloss", [False, True])
+def test_fused_loss_other_action_widths_gpu(n_act, clip_vloss):
+    """The other widths vss_ppo_loss is built for (N_ACT): the same checks as the Agent's 2 and 6."""
+    _check_fused_loss(n_act, clip_vloss, True)
+
+
+@pytest.mark.gpu
+def test_fused_loss_refuses_inputs_the_kernel_would_misread_gpu():
+    """Fewer action rows than network rows (the kernel would read past the buffer), or an input that is
+    not fp32 on the networks' device (it would be reinterpreted as fp32 device memory): ValueError."""
+    ins = list(_inputs(1000, 24, 2, 5, "cuda", True))
+    bad = list(ins)
+    bad[3] = ins[3][:1010]
+    with pytest.raises(ValueError):
+        ppo_loss(*bad, 0.2, 0.005, 4.0, False)
+    for k in range(4, 8):
+        for t in (ins[k].double(), ins[k].cpu()):
+            bad = list(ins)
+            bad[k] = t
+            with pytest.raises(ValueError):
+                ppo_loss(*bad, 0.2, 0.005, 4.0, False)
+
+
+def _check_fused_loss(n_act, clip_vloss, norm_adv):
     rows, pad = 131040, 224
     ins = _inputs(rows, pad, n_act, 7 + n_act + 2 * clip_vloss, "cuda", norm_adv)
     coef = (0.2, 0.005, 4.0, clip_vloss)

@@ -3,6 +3,7 @@ GAE known answers, the flat-gradient data-parallel update (gloo, world size 2, C
 end-to-end training run on the GPU."""
 import os
 import socket
+import warnings
 from collections import namedtuple
 
 import numpy as np
@@ -229,15 +230,40 @@ def test_minibatch_graph_update_equals_eager_gpu(n, nmb, epochs, updates, norm_a
         assert {k: float(v) for k, v in a.items()} == {k: float(v) for k, v in b.items()}
 
 
+def test_graph_check_schedule_is_geometric():
+    """The captured minibatch is re-checked against eager at replays 12, 48, 192, ... (not once)."""
+    due = [r for r in range(1, 4000) if P.graph_check_due(r)]
+    assert due == [12, 48, 192, 768, 3072]
+
+
+def test_no_capture_when_packet_capture_is_on(monkeypatch):
+    """A runtime started with graph packet capture on (switch unset or not "0") gets no captured
+    minibatch: make_minibatch_graph warns once and returns None, so the update runs eagerly."""
+    args = _args(norm_adv=True, clip_vloss=False, num_minibatches=4, update_epochs=1)
+    monkeypatch.setattr(P, "_WARNED_PACKET_CAPTURE", [False])
+    for value in (None, "1"):
+        if value is None:
+            monkeypatch.delenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE", raising=False)
+        else:
+            monkeypatch.setenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE", value)
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            assert P.make_minibatch_graph(None, None, args, 1024, (52,), (2,), "cuda") is None
+        assert len(w) == (1 if value is None else 0)  # once per process
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("corrupt", [False, True])
+@pytest.mark.parametrize("corrupt", [None, "first", "later"])
 def test_minibatch_graph_self_check_gpu(corrupt):
-    """MinibatchGraph re-runs replay GRAPH_CHECK_REPLAY eagerly and compares the two bit for bit.  A
-    healthy graph passes and stays in use; a replay whose gradients are corrupted (here: injected into
-    FlatGrads after that replay) is caught, the minibatch takes the eager result, the graph is dropped
-    and the rest of the update runs eagerly -- the update then equals the eager one exactly."""
-    args = _args(norm_adv=True, clip_vloss=False, num_minibatches=4, update_epochs=4)  # 16 minibatches
+    """MinibatchGraph re-runs replays 12, 48, ... eagerly and compares each bit for bit.  A healthy graph
+    passes and stays in use; a replay whose gradients are corrupted (here: injected into FlatGrads after
+    the replay) is caught -- at the first check, or at the second when the corruption starts after the
+    first -- the minibatch takes the eager result, the graph is dropped and the rest of the update runs
+    eagerly: the update then equals the eager one exactly."""
+    # 4 minibatches x 13 epochs = 52 minibatches: replays 1 .. 51 cover the checks at 12 and 48
+    args = _args(norm_adv=True, clip_vloss=False, num_minibatches=4, update_epochs=13)
     n = 32768
+    bad_replay = {None: None, "first": P.GRAPH_CHECK_REPLAY, "later": P.GRAPH_CHECK_REPLAY * P.GRAPH_CHECK_FACTOR}[corrupt]
     obs, act, logp, adv, ret, val = [t.cuda() for t in _synthetic_batch(5, n)]
     res = []
     for use_graph in (False, True):
@@ -245,16 +271,24 @@ def test_minibatch_graph_self_check_gpu(corrupt):
         flat = P.FlatGrads(agent)
         opt = torch.optim.Adam(agent.parameters(), lr=1e-3, eps=1e-5)
         graph = P.make_minibatch_graph(agent, flat, args, n, (52,), (2,), "cuda") if use_graph else None
+        checks = []
+        if graph is not None:
+            check = graph._check
+
+            def counting_check():
+                checks.append(graph.replays)
+                return check()
+            graph._check = counting_check
         if graph is not None and corrupt:
             capture = graph._capture
 
-            class Corrupting:  # the captured graph, with a wrong gradient after the checked replay
+            class Corrupting:  # the captured graph, with a wrong gradient after the replay bad_replay
                 def __init__(self, g):
                     self.g = g
 
                 def replay(self):
                     self.g.replay()
-                    if graph.replays + 1 == P.GRAPH_CHECK_REPLAY:
+                    if graph.replays + 1 >= bad_replay:
                         flat.flat[7] += 1.0
 
             def capture_and_corrupt():
@@ -269,8 +303,10 @@ def test_minibatch_graph_self_check_gpu(corrupt):
             P.ppo_update(agent, opt, flat, args, obs, logp, act, adv, ret, val, gen=gen, graph=graph)
         res.append(torch.cat([p.detach().reshape(-1) for p in agent.parameters()]))
         if graph is not None:
-            assert graph.replays >= P.GRAPH_CHECK_REPLAY
-            assert graph.failed == corrupt and (graph.graph is None) == corrupt
+            assert graph.failed == bool(corrupt) and (graph.graph is None) == bool(corrupt)
+            assert checks == ([12, 48] if corrupt in (None, "later") else [12]), checks
+            if corrupt is None:
+                assert graph.replays == 51
     assert torch.equal(res[0], res[1])
 
 

@@ -71,11 +71,8 @@ def test_cpu_fused_layer_formulas_match_autograd():
     torch.testing.assert_close(db, ref.sum(0), rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("mlp", ["fused", "split"])
-def test_update_mlp_paths_cpu_match_autograd(mlp, monkeypatch):
-    """Both update MLP paths (the _TanhMLP node and the per-layer functions) on CPU tensors: the
-    Agent's outputs and autograd's gradients."""
-    monkeypatch.setattr(P, "UPDATE_MLP", mlp)
+def test_update_mlp_path_cpu_matches_autograd():
+    """The update's MLP node (_TanhMLP) on CPU tensors: the Agent's outputs and autograd's gradients."""
     agent = make_agent(2)
     g = torch.Generator().manual_seed(5)
     x = torch.randn(96, 52, generator=g)
@@ -215,16 +212,14 @@ def test_fused_gemm_refusals_gpu():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("act_dim", [2, 6])
-@pytest.mark.parametrize("mlp,gemm", [("fused", "x6"), ("fused", "fp32"), ("split", "x6")])
+@pytest.mark.parametrize("gemm", ["x6", "fp32"])
 @pytest.mark.parametrize("rows", [256, 65536 + 64 * 3])
-def test_update_gradients_through_hip_match_autograd_gpu(rows, mlp, gemm, act_dim, monkeypatch):
-    """The update's forward equals the Agent's (bit for bit on the hipBLASLt path "split"; within
-    fp32 GEMM rounding on the fused-GEMM path, with the bf16x6 GEMMs where the shapes are exact --
-    all of them at 256 rows, the weight gradients only at 65,728 -- or the fp32-MFMA ones); its
-    gradients (fused HIP GEMM epilogues or the HIP tanh backward + bias, split-K dW) equal autograd's
-    up to fp32 summation order.  act_dim 6 (the CMA actor: 6 output columns padded to k_pad = 8 in
+def test_update_gradients_through_hip_match_autograd_gpu(rows, gemm, act_dim, monkeypatch):
+    """The update's forward equals the Agent's within fp32 GEMM rounding (the bf16x6 GEMMs where the
+    shapes are exact -- all of them at 256 rows, the weight gradients only at 65,728 -- or the fp32-MFMA
+    ones); its gradients (fused HIP GEMM epilogues, split weight gradients) equal autograd's up to fp32
+    summation order.  act_dim 6 (the CMA actor: 6 output columns padded to k_pad = 8 in
     vss_output_backward) as well as 2 (SA/DMA: k_pad = 4; the 1-column critic pads to 4 in both)."""
-    monkeypatch.setattr(P, "UPDATE_MLP", mlp)
     monkeypatch.setattr(P, "UPDATE_GEMM", gemm)
     agent = make_agent(act_dim).cuda()
     g = torch.Generator(device="cuda").manual_seed(3)
@@ -234,7 +229,7 @@ def test_update_gradients_through_hip_match_autograd_gpu(rows, mlp, gemm, act_di
     loss_ref = outs_ref[1].sum() + outs_ref[2].sum() + outs_ref[3].sum()
     grads_ref = torch.autograd.grad(loss_ref, list(agent.parameters()))
     outs = P.get_action_and_value_update(agent, x, a)
-    tol = 0 if mlp == "split" else 2e-5
+    tol = 2e-5
     for u, v in zip(outs[1:], outs_ref[1:]):
         torch.testing.assert_close(u, v, rtol=tol, atol=tol)
     loss = outs[1].sum() + outs[2].sum() + outs[3].sum()
@@ -335,27 +330,3 @@ def test_update_gradients_on_rollout_data_at_fp32_error_gpu():
         ea = float((a - c).norm() / c.norm())
         eb = float((b - c).norm() / c.norm())
         assert ea <= (1.25 if eb >= 1e-6 else 2.0) * eb + 1e-9 and ea < 1e-5, (name, ea, eb)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("out_fwd,out_bwd", [(False, True), (True, False), (False, False)])
-def test_output_layer_ab_switches_match_autograd_gpu(out_fwd, out_bwd, monkeypatch):
-    """The A/B switches of _TanhMLP's output layer (VSS_OUTPUT_FWD=0: a separate addmm instead of the
-    folded epilogue; VSS_OUTPUT_BWD=0: the padded backward GEMM + split-K dW instead of the one-pass
-    vss_output_backward) compute the same function and gradients as autograd (fp32 tolerances of
-    test_update_gradients_through_hip_match_autograd_gpu)."""
-    monkeypatch.setattr(P, "OUTPUT_FWD", out_fwd)
-    monkeypatch.setattr(P, "OUTPUT_BWD", out_bwd)
-    agent = make_agent(2).cuda()
-    g = torch.Generator(device="cuda").manual_seed(4)
-    rows = 65536
-    x = torch.randn(rows, 52, device="cuda", generator=g)
-    a = torch.randn(rows, 2, device="cuda", generator=g) * 0.5
-    outs_ref = agent.get_action_and_value(x, a)
-    grads_ref = torch.autograd.grad(outs_ref[1].sum() + outs_ref[3].sum(), list(agent.parameters()))
-    outs = P.get_action_and_value_update(agent, x, a)
-    for u, v in zip(outs[1:], outs_ref[1:]):
-        torch.testing.assert_close(u, v, rtol=2e-5, atol=2e-5)
-    grads = torch.autograd.grad(outs[1].sum() + outs[3].sum(), list(agent.parameters()))
-    for (name, _), u, v in zip(agent.named_parameters(), grads, grads_ref):
-        torch.testing.assert_close(u, v, rtol=2e-4, atol=2e-4 * float(v.abs().max()) + 1e-6, msg=name)

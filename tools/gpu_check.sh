@@ -52,6 +52,7 @@ case ",$STEPS," in *,gemm,*)
   run pytest_update 500 python -u -m pytest tests/test_update.py -m gpu -x -v --timeout 120 --timeout-method thread
   run gemm_fused 300 python -u tools/gemm_fused_bench.py
   VSS_UPDATE_MLP=fused run ppo_fused 300 python -u rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 3 --log false
+  # (needs tools/ab_switches_r04.patch applied: the split path is retired from the product)
   VSS_UPDATE_MLP=split run ppo_split 300 python -u rsoccer-isaac-cleanrl_amd/ppo_continuous_action_isaacgym.py --env-id sa --num-envs 65536 --num-updates 3 --log false ;;
 esac
 case ",$STEPS," in *,sa1e8,*)

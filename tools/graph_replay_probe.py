@@ -13,7 +13,7 @@ Stages (STAGES, comma separated), each captured and replayed REPLAYS times:
   minibatch MinibatchGraph's body (forward, losses, backward into FlatGrads)
 
 PATH_MLP selects the update's MLP arithmetic: x6 (default product), fp32 (VSS_UPDATE_GEMM=fp32), split
-(VSS_UPDATE_MLP=split: hipBLASLt + vss_tanh_grad_bias), torch (plain nn.Sequential); LOSS selects the
+(VSS_UPDATE_MLP=split: hipBLASLt + vss_tanh_grad_bias; needs tools/ab_switches_r04.patch applied), torch (plain nn.Sequential); LOSS selects the
 minibatch loss: fused (vss_ppo_loss, default) or torch (the reference's expressions).  PATH_MLP=torch
 LOSS=torch puts no kernel of this repository in the graph.  Set DEBUG_CLR_GRAPH_PACKET_CAPTURE on the
 command line.  NOISE > 0 launches that many tiny eager kernels after each replay; stage ppo runs the
@@ -26,7 +26,7 @@ sys.path.insert(0, os.path.join(REPO, "rsoccer-isaac-cleanrl_amd"))
 PATH = os.environ.get("PATH_MLP", "x6")
 if PATH == "fp32":
     os.environ["VSS_UPDATE_GEMM"] = "fp32"
-if PATH == "split":
+if PATH == "split":  # retired from the product in round 5: apply tools/ab_switches_r04.patch first
     os.environ["VSS_UPDATE_MLP"] = "split"
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -15,9 +15,14 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import ppo_continuous_action_isaacgym as P  # noqa: E402
+
+PACKET_CAPTURE_OFF = P.disable_graph_packet_capture()  # an entry point: before anything initialises the GPU
 from envs._gym import Box  # noqa: E402
 from vss_amd import _native as N  # noqa: E402
 from vss_amd.policy import FusedPolicy  # noqa: E402
+
+
+print(f"DEBUG_CLR_GRAPH_PACKET_CAPTURE off: {PACKET_CAPTURE_OFF}", flush=True)
 
 
 def timeit(fn, iters=20):

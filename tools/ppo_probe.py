@@ -11,6 +11,8 @@ import torch  # noqa: E402
 
 import ppo_continuous_action_isaacgym as P  # noqa: E402
 
+PACKET_CAPTURE_OFF = P.disable_graph_packet_capture()  # an entry point: before anything initialises the GPU
+
 if os.environ.get("PROBE_ENV", "0") == "1":
     from envs.vss import VSS, default_cfg
     env = VSS(default_cfg(65536), "cuda:0", "cuda:0", 0, True, False, False)
@@ -23,5 +25,5 @@ args = P.parse_args(["--env-id", os.environ.get("ENV_ID", "sa"), "--num-envs", o
 _, hist = P.train(args)
 for h in hist:
     if "update_s" in h:
-        print(f"PROBE_ENV={os.environ.get('PROBE_ENV', '0')} log={args.log} update {h['update']} rollout {h['rollout_s']:.3f} "
+        print(f"PROBE_ENV={os.environ.get('PROBE_ENV', '0')} packet_capture_off={PACKET_CAPTURE_OFF} log={args.log} update {h['update']} rollout {h['rollout_s']:.3f} "
               f"update {h['update_s']:.3f}", flush=True)

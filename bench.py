@@ -317,6 +317,13 @@ def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
     walls = reduce_max([h["wall_s"] for h in hist], red)
     per_update = roll_s + upd_s
     batch = args.batch_size * world
+    # steady state vs first use: each update's share of the train clock (max over ranks); the steady
+    # figure is the median over updates 2.. (the first carries the first kernel uses, the graph capture
+    # and the env reset); the 1e8 wall-clock at N GPUs = first update + (updates - 1) x steady, so the
+    # scaling of train throughput is read from steady_train_env_steps_per_s, not from the 1e8 clock
+    # (quantised: 12 updates at 1 GPU, 2 at 8)
+    deltas = [walls[0]] + [b - a for a, b in zip(walls, walls[1:])]
+    steady = float(np.median(deltas[1:])) if len(deltas) > 1 else None
     updates_1e8 = ppo_updates_to_1e8(n_envs, world, args.num_steps)
     reached = next((i for i, h in enumerate(hist) if h["global_step"] >= 1e8), None)
     ref_updates = int(1e8) // batch  # the reference's num_updates for --total-timesteps 1e8 (ppo…:247)
@@ -342,6 +349,14 @@ def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
             "wall_s_per_update": walls, "train_call_s": call_s,
             "rollout_s": roll_s, "update_s": upd_s, "timed_update": len(hist),
             "rollout_env_steps_per_s": batch / roll_s, "train_env_steps_per_s": batch / per_update,
+            "steady_s_per_update": steady,
+            "steady_train_env_steps_per_s": batch / steady if steady else None,
+            "first_update_s": deltas[0],
+            "first_update_overhead_s": deltas[0] - steady if steady else None,
+            "steady_state_note": ("steady = median of the per-update train-clock deltas after the first (max over "
+                                  "ranks); first_update_overhead_s = the first update's delta minus it (env reset, first "
+                                  "kernel uses, the minibatch graph capture); nothing is run before the train clock "
+                                  "starts (ppo…:244) besides what the reference also does there (env and Agent creation)"),
             "projected_wallclock_to_1e8_steps_s": updates_1e8 * per_update, "updates_to_1e8": updates_1e8}
 
 

@@ -356,6 +356,13 @@ int vss_output_backward(void* stream, int64_t rows, int32_t k_pad, int32_t n, co
  * vss_weight_grad_chunks_bf16x6(rows, n_out, k_in) parts (-1 for a bad shape).  rows % 64 == 0,
  * n_out % 256 == 0, k_in % 128 == 0; every pointer 16-B aligned.  Replaces hipBLASLt's split-K
  * grad^T x GEMM.
+ *
+ * vss_first_weight_grad_bf16x6: the same for the Agent's FIRST layer (nn.Linear(obs, 256),
+ * ppo_continuous_action_isaacgym.py:131,142; its weight gradient under loss.backward(), ppo…:352),
+ * whose input x (rows, k_in) is the observation: n_out == 256, k_in <= 64 and k_in % 4 == 0 (52 for
+ * every VSS wrapper), rows % 64 == 0; grad and x 16-B aligned.  partial (parts, 256, k_in), parts =
+ * vss_first_weight_grad_chunks_bf16x6(rows, n_out, k_in) (-1 for a bad shape).  Replaces hipBLASLt's
+ * batched grad^T x + torch.sum (the split-K dW of the first layer).
  * ------------------------------------------------------------------------------------------- */
 int vss_linear_tanh_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
                            const float* bias, float* y, uint16_t* w_split);
@@ -371,6 +378,9 @@ int vss_weight_planes_bf16x6(void* stream, int32_t count, const float* const* w,
 int64_t vss_weight_grad_chunks_bf16x6(int64_t rows, int32_t n_out, int32_t k_in);
 int vss_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_in, const float* grad, const float* x,
                            float* partial);
+int64_t vss_first_weight_grad_chunks_bf16x6(int64_t rows, int32_t n_out, int32_t k_in);
+int vss_first_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_in, const float* grad,
+                                 const float* x, float* partial);
 
 /* ---------------------------------------------------------------------------------------------
  * The clipped PPO loss of one update minibatch and its gradients (SURVEY §8 A13;

@@ -643,6 +643,176 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
   }
 }
 
+// ---- the first layer's weight gradient: dW (256, k_in <= 64) = grad^T x over all rows ----------------
+// The Agent's first Linear (52 -> 256, ppo…:131,142) under loss.backward() (ppo…:352): grad (rows, 256)
+// is the first tanh layer's pre-activation gradient, x (rows, k_in) the observations.  A block of 4 waves
+// takes a contiguous range of K tiles (32 rows each) and accumulates the whole (256, 64) tile, wave w the
+// features 64 w .. 64 w + 63 (4 x 4 MFMA tiles); the grid's parts are summed by the caller.  The bytes are
+// the operands once (HBM-bound: 1,024 + 4 k_in B per row); the six products keep it well under that roof.
+//   grad: the K tile's 32 x 256 floats (32 KB contiguous) staged as ST_KROW into a KImg<256> image;
+//   x:    its 32 x k_in floats (contiguous, k_in % 4 == 0) as 16-B chunks of 4 columns, in a 4 KB-per-plane
+//         image of 16 LDS rows x 128 features: contraction row r sits at LDS row r & 15, feature
+//         c + 64 (r >> 4), the 16-B chunks XOR-swizzled by kswz(row) as in KImg -- so the transposed
+//         fragment reads are those of KImg (16 distinct 16-B slots per 32-lane half).  Columns k_in .. 63
+//         stay zero (written once).
+constexpr int FW_THREADS = 256, FW_N = 256, FW_KMAX = 64;
+constexpr int FW_XPS = 16 * 256;                         // x image bytes per plane
+constexpr int FW_GPS = KImg<FW_N>::PS;                   // grad image bytes per plane
+constexpr int FW_BUF = 3 * FW_GPS + 3 * FW_XPS;          // 60 KB
+constexpr int FW_NX = (32 * FW_KMAX / 4) / FW_THREADS;   // x chunks per thread (2)
+
+// byte offset in one x plane of contraction row r, feature column c (c % 4 == 0): the 8-B piece of c .. c + 3
+__device__ __forceinline__ int fw_xoff(int r, int c) {
+  const int rho = r & 15, phi = c + 64 * (r >> 4);
+  return rho * 256 + 16 * ((phi >> 3) ^ kswz(rho)) + 8 * ((phi >> 2) & 1);
+}
+
+__global__ __launch_bounds__(FW_THREADS, 1) void first_wgrad_kernel(int64_t kpairs, int32_t k_in, const float* __restrict__ grad,
+                                                                      const float* __restrict__ x, float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * FW_BUF];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int G = gridDim.x, b = blockIdx.x;
+  // this block's K tiles: parts differ by at most one K-tile pair
+  const int64_t kt0 = 2 * ((int64_t)b * kpairs / G), kn = 2 * (((int64_t)b + 1) * kpairs / G) - kt0;
+  const int xchunks = 8 * k_in;  // 16-B chunks of one K tile of x
+  // zero both x images once: the columns k_in .. 63 are never written
+  for (int i = tid; i < 2 * 3 * FW_XPS / 16; i += FW_THREADS) {
+    const int buf = i / (3 * FW_XPS / 16), o = i % (3 * FW_XPS / 16);
+    *reinterpret_cast<u32x4*>(lds + buf * FW_BUF + 3 * FW_GPS + 16 * o) = (u32x4){0u, 0u, 0u, 0u};
+  }
+  struct St {
+    u32x4 g[4][2];
+    u32x4 x[FW_NX];
+  };
+  int64_t f_kt = 0;
+  auto gload = [&](St& s) {
+    const int64_t kt = kt0 + (f_kt < kn ? f_kt : kn - 1);  // past the last: re-load it (in bounds, unused)
+    ++f_kt;
+    const float* gsrc = grad + kt * 32 * FW_N;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int pr = tid + FW_THREADS * u, row = pr >> 5, cc = pr & 31;  // 8 consecutive features of one row
+      s.g[u][0] = *reinterpret_cast<const u32x4*>(gsrc + row * FW_N + 8 * cc);
+      s.g[u][1] = *reinterpret_cast<const u32x4*>(gsrc + row * FW_N + 8 * cc + 4);
+    }
+    const float* xsrc = x + kt * 32 * k_in;
+#pragma unroll
+    for (int u = 0; u < FW_NX; ++u) {
+      const int ch = tid + FW_THREADS * u;
+      if (ch < xchunks) s.x[u] = *reinterpret_cast<const u32x4*>(xsrc + 4 * ch);
+    }
+  };
+  auto swrite = [&](const St& s, int buf) {
+    char* gimg = lds + buf * FW_BUF;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int pr = tid + FW_THREADS * u, row = pr >> 5, cc = pr & 31;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(s.g[u][e >> 2][e & 3]);
+      u32x4 hi, mid, lo;
+      split8(v, hi, mid, lo);
+      char* d = gimg + (cc >> 4) * KImg<FW_N>::SUB + row * 256 + 16 * ((cc & 15) ^ kswz(row));
+      *reinterpret_cast<u32x4*>(d) = hi;
+      *reinterpret_cast<u32x4*>(d + FW_GPS) = mid;
+      *reinterpret_cast<u32x4*>(d + 2 * FW_GPS) = lo;
+    }
+    char* ximg = lds + buf * FW_BUF + 3 * FW_GPS;
+    const int cpr = k_in >> 2;  // chunks per row
+#pragma unroll
+    for (int u = 0; u < FW_NX; ++u) {
+      const int ch = tid + FW_THREADS * u;
+      if (ch < xchunks) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = __uint_as_float(s.x[u][e]);
+          v[4 + e] = 0.f;
+        }
+        u32x4 hi, mid, lo;
+        split8(v, hi, mid, lo);
+        char* d = ximg + fw_xoff(ch / cpr, 4 * (ch % cpr));
+        *reinterpret_cast<uint2*>(d) = (uint2){hi[0], hi[1]};
+        *reinterpret_cast<uint2*>(d + FW_XPS) = (uint2){mid[0], mid[1]};
+        *reinterpret_cast<uint2*>(d + 2 * FW_XPS) = (uint2){lo[0], lo[1]};
+      }
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int q = (lane >> 2) & 3, p = lane & 3, fg = lane >> 4;
+  auto mfma_tile = [&](int buf) {
+    const char* gk = lds + buf * FW_BUF;
+    const char* xk = lds + buf * FW_BUF + 3 * FW_GPS;
+    u32x4 pf[3][4], qf[3][4];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int i0 = 64 * wv + 16 * i;
+        pf[pl][i] = tr_frag(gk + pl * FW_GPS + kfrag_off(i0, lane, 0), gk + pl * FW_GPS + kfrag_off(i0, lane, 1));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // contraction rows 8 fg + 4 h + q, columns 16 j + 4 p .. + 3
+        const int r0 = 8 * fg + q;
+        qf[pl][j] = tr_frag(xk + pl * FW_XPS + fw_xoff(r0, 16 * j + 4 * p), xk + pl * FW_XPS + fw_xoff(r0 + 4, 16 * j + 4 * p));
+      }
+    }
+    constexpr int PP[6] = {2, 0, 1, 1, 0, 0};
+    constexpr int QP[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+    for (int xx = 0; xx < 6; ++xx)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pf[PP[xx]][i]),
+                                                              __builtin_bit_cast(bf16x8, qf[QP[xx]][j]), acc[i][j], 0, 0, 0);
+  };
+  St r0, r1;
+  __syncthreads();  // the zeroed x images before any staging write lands beside them
+  gload(r0);
+  swrite(r0, 0);
+  gload(r1);
+  gload(r0);
+  __syncthreads();
+  for (int64_t kt = 0; kt < kn; kt += 2) {
+    mfma_tile(0);
+    swrite(r1, 1);
+    __syncthreads();
+    gload(r1);
+    mfma_tile(1);
+    swrite(r0, 0);
+    __syncthreads();
+    gload(r0);
+  }
+  // lane holds D[f = 64 wv + 16 i + 4 fg + r][c = 16 j + fr]; columns past k_in are zero and not stored
+  const int fr = lane & 15;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = 16 * j + fr;
+    if (c < k_in) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) partial[((int64_t)b * FW_N + 64 * wv + 16 * i + 4 * fg + r) * k_in + c] = acc[i][j][r];
+    }
+  }
+}
+
+// parts: enough K-tile pairs per block to amortise its epilogue (>= 8 pairs), at most one block per CU
+static int fw_parts(int64_t rows) {
+  const int64_t pairs = rows / (2 * KT);
+  int64_t g = pairs / 8;
+  if (g > 256) g = 256;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
 constexpr int kGridCus = 256;  // persistent grid sized for MI355X on every device (fixed partial layout)
 
 struct Plan {
@@ -849,6 +1019,25 @@ int vss_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_
   a.ldo = k_in;
   a.out = partial;
   return launch<EPI_WGRAD, ST_KROW, ST_KROW, CfgA>(stream, a, wg_plan(rows, n_out, k_in));
+}
+
+int64_t vss_first_weight_grad_chunks_bf16x6(int64_t rows, int32_t n_out, int32_t k_in) {
+  using namespace vx6;
+  if (rows <= 0 || rows % (2 * KT) || rows > (int64_t(1) << 36) || n_out != FW_N || k_in <= 0 || k_in > FW_KMAX ||
+      k_in % 4)
+    return -1;
+  return fw_parts(rows);
+}
+
+int vss_first_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_in, const float* grad,
+                                 const float* x, float* partial) {
+  using namespace vx6;
+  if (vss_first_weight_grad_chunks_bf16x6(rows, n_out, k_in) < 0 || misaligned(grad) || misaligned(x) || !partial)
+    return VSS_E_ARG;
+  const int g = fw_parts(rows);
+  hipLaunchKernelGGL(first_wgrad_kernel, dim3((unsigned)g), dim3(FW_THREADS), 0, (hipStream_t)stream,
+                     (int64_t)(rows / (2 * KT)), k_in, grad, x, partial);
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 
 }  // extern "C"

@@ -56,7 +56,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from envs._gym import Box, ObservationWrapper  # noqa: E402
 from vss_amd.loss import ppo_loss  # noqa: E402
-from vss_amd.update import (gemm_shape_ok, linear_tanh, linear_tanh_backward, linear_tanh_backward_mixed,  # noqa: E402
+from vss_amd.update import (first_wgrad_ok, gemm_shape_ok, linear_tanh, linear_tanh_backward, linear_tanh_backward_mixed,  # noqa: E402
                             linear_tanh_mixed, linear_tanh_out, linear_tanh_out_mixed, linear_tanh_out_ok,
                             output_backward, output_backward_ok, weight_grad_mixed, weight_planes,
                             x6_ok)
@@ -245,7 +245,9 @@ class _TanhMLP(torch.autograd.Function):
                                                            out_dw=dst[2 * layer])
                 continue
             x6 = gz.is_cuda and UPDATE_GEMM == "x6"
-            if x6 and hs[layer].shape[1] % 128 == 0 and gz.shape[1] % 256 == 0:
+            if x6 and ((hs[layer].shape[1] % 128 == 0 and gz.shape[1] % 256 == 0) or
+                       (layer == 0 and first_wgrad_ok(256, gz.shape[1], hs[0].shape[1]))):
+                # the hidden layers' and the first layer's weight gradients on the x6 kernels
                 grads[2 * layer] = weight_grad_mixed(gz, hs[layer], out=dst[2 * layer])
             else:
                 grads[2 * layer] = _split_k_wgrad(gz, hs[layer], out=dst[2 * layer])

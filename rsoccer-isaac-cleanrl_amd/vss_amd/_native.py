@@ -38,7 +38,8 @@ EXPORTED = ("vss_abi_version", "vss_source_hash", "vss_error_string", "vss_step"
             "vss_linear_tanh", "vss_linear_tanh_out", "vss_linear_tanh_backward_chunks", "vss_linear_tanh_backward",
             "vss_output_backward_chunks", "vss_output_backward", "vss_linear_tanh_bf16x6",
             "vss_linear_tanh_out_bf16x6", "vss_linear_tanh_backward_chunks_bf16x6", "vss_linear_tanh_backward_bf16x6",
-            "vss_weight_grad_chunks_bf16x6", "vss_weight_grad_bf16x6", "vss_weight_planes_bf16x6", "vss_ppo_loss_scratch_floats", "vss_ppo_loss")
+            "vss_weight_grad_chunks_bf16x6", "vss_weight_grad_bf16x6", "vss_first_weight_grad_chunks_bf16x6",
+            "vss_first_weight_grad_bf16x6", "vss_weight_planes_bf16x6", "vss_ppo_loss_scratch_floats", "vss_ppo_loss")
 
 
 class VssParams(ctypes.Structure):
@@ -173,6 +174,10 @@ def load() -> ctypes.CDLL:
     L.vss_weight_grad_chunks_bf16x6.restype = i64
     L.vss_weight_grad_bf16x6.argtypes = [P, i64, i32, i32, P, P, P]
     L.vss_weight_grad_bf16x6.restype = ctypes.c_int
+    L.vss_first_weight_grad_chunks_bf16x6.argtypes = [i64, i32, i32]
+    L.vss_first_weight_grad_chunks_bf16x6.restype = i64
+    L.vss_first_weight_grad_bf16x6.argtypes = [P, i64, i32, i32, P, P, P]
+    L.vss_first_weight_grad_bf16x6.restype = ctypes.c_int
     L.vss_weight_planes_bf16x6.argtypes = [P, i32, P, P, P, P, P]
     L.vss_weight_planes_bf16x6.restype = ctypes.c_int
     f32 = ctypes.c_float

@@ -241,13 +241,17 @@ def _x6_check(name, cond, *ts):
 
 
 def _w_and_planes(w: torch.Tensor, planes: torch.Tensor | None):
-    """(weight pointer, planes pointer) for an x6 entry: the entry splits w itself (planes None), or
-    takes the weight_planes() result with a NULL weight."""
+    """(weight pointer, planes pointer, keep) for an x6 entry: the entry splits w itself (planes None),
+    or takes the weight_planes() result with a NULL weight.  `keep` holds the tensors behind the pointers
+    (w, e.g. a transposed copy, and the planes scratch): the caller keeps it until its launch is queued,
+    so that no allocation in between (the output, the partial sums) can take their memory while the
+    split and the GEMM still use it."""
     if planes is None:
-        return w.data_ptr(), _planes(w).data_ptr()
+        scratch = _planes(w)
+        return w.data_ptr(), scratch.data_ptr(), (w, scratch)
     if planes.dtype != torch.int16 or planes.numel() != 3 * w.numel():
         raise ValueError(f"planes: weight_planes() output of this weight, got {planes.dtype} {tuple(planes.shape)}")
-    return None, planes.data_ptr()
+    return None, planes.data_ptr(), (planes,)
 
 
 def linear_tanh_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
@@ -259,9 +263,10 @@ def linear_tanh_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch
     _x6_check("vss_linear_tanh_bf16x6", w.shape == (n, k) and b.shape == (n,) and x6_ok(rows, k, n), x, w, b)
     x, w, b = x.contiguous(), w.contiguous(), b.contiguous()
     y = _out(out, (rows, n), x)
-    wp, pp = _w_and_planes(w, planes)
+    wp, pp, keep = _w_and_planes(w, planes)
     N.check(N.load().vss_linear_tanh_bf16x6(N.stream_of(x.device), rows, k, n, x.data_ptr(), wp,
                                             b.data_ptr(), y.data_ptr(), pp), "vss_linear_tanh_bf16x6")
+    del keep  # the split and the GEMM are queued: the scratch may be reused from here on
     return y
 
 
@@ -275,10 +280,11 @@ def linear_tanh_out_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out:
     x, w, b, w_out = x.contiguous(), w.contiguous(), b.contiguous(), w_out.contiguous()
     y = _out(out, (rows, n), x)
     part = torch.empty((n // 64, rows, k_out), device=x.device, dtype=torch.float32)
-    wp, pp = _w_and_planes(w, planes)
+    wp, pp, keep = _w_and_planes(w, planes)
     N.check(N.load().vss_linear_tanh_out_bf16x6(N.stream_of(x.device), rows, k, n, x.data_ptr(), wp,
                                                 b.data_ptr(), y.data_ptr(), k_out, w_out.data_ptr(), part.data_ptr(),
                                                 pp), "vss_linear_tanh_out_bf16x6")
+    del keep  # the split and the GEMM are queued: the scratch may be reused from here on
     return y, part.sum(0).add_(b_out)
 
 
@@ -294,15 +300,16 @@ def linear_tanh_backward_x6(gz_next: torch.Tensor, w_next: torch.Tensor, y: torc
     lib = N.load()
     gz_next, y = gz_next.contiguous(), y.contiguous()
     if planes is None:
-        wp, pp = _w_and_planes(w_next.t().contiguous(), None)  # (n, k_next): K-contiguous
+        wp, pp, keep = _w_and_planes(w_next.t().contiguous(), None)  # (n, k_next): K-contiguous
     else:
-        wp, pp = _w_and_planes(w_next, planes)
+        wp, pp, keep = _w_and_planes(w_next, planes)
     gz = _out(out, (rows, n), y)
     partial = torch.empty((lib.vss_linear_tanh_backward_chunks_bf16x6(rows, k_next, n), n), device=y.device,
                           dtype=torch.float32)
     N.check(lib.vss_linear_tanh_backward_bf16x6(N.stream_of(y.device), rows, k_next, n, gz_next.data_ptr(),
                                                 wp, y.data_ptr(), gz.data_ptr(), partial.data_ptr(), pp),
             "vss_linear_tanh_backward_bf16x6")
+    del keep  # the split and the GEMM are queued: the scratch may be reused from here on
     return gz, torch.sum(partial, 0, out=out_db)
 
 
@@ -319,6 +326,28 @@ def weight_grad_x6(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None
                         dtype=torch.float32)
     N.check(lib.vss_weight_grad_bf16x6(N.stream_of(x.device), rows, n_out, k_in, grad.data_ptr(), x.data_ptr(),
                                        parts.data_ptr()), "vss_weight_grad_bf16x6")
+    return torch.sum(parts, 0, out=out)
+
+
+def first_wgrad_ok(rows: int, n_out: int, k_in: int) -> bool:
+    """Shapes vss_first_weight_grad_bf16x6 takes (the Agent's first layer): n_out 256, k_in <= 64 and
+    k_in % 4 == 0, rows % 64."""
+    return rows > 0 and rows % 64 == 0 and n_out == 256 and 0 < k_in <= 64 and k_in % 4 == 0
+
+
+def first_weight_grad_x6(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """dW = grad.T @ x for the Agent's first layer (grad (rows, 256), x (rows, k_in <= 64): the
+    observations) on the bf16 matrix cores with fp32 arithmetic, split over the rows
+    (vss_first_weight_grad_bf16x6); the parts are reduced into `out` when given."""
+    rows, n_out = grad.shape
+    k_in = x.shape[1]
+    _x6_check("vss_first_weight_grad_bf16x6", x.shape[0] == rows and first_wgrad_ok(rows, n_out, k_in), grad, x)
+    lib = N.load()
+    grad, x = grad.contiguous(), x.contiguous()
+    parts = torch.empty((lib.vss_first_weight_grad_chunks_bf16x6(rows, n_out, k_in), n_out, k_in), device=x.device,
+                        dtype=torch.float32)
+    N.check(lib.vss_first_weight_grad_bf16x6(N.stream_of(x.device), rows, n_out, k_in, grad.data_ptr(), x.data_ptr(),
+                                             parts.data_ptr()), "vss_first_weight_grad_bf16x6")
     return torch.sum(parts, 0, out=out)
 
 
@@ -378,13 +407,19 @@ def linear_tanh_backward_mixed(gz_next: torch.Tensor, w_next: torch.Tensor, y: t
 
 
 def weight_grad_mixed(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """out: where to reduce the weight gradient into (the same tensor returned)."""
+    """out: where to reduce the weight gradient into (the same tensor returned).  The hidden layers'
+    shapes on vss_weight_grad_bf16x6, the first layer's (x = the observations) on
+    vss_first_weight_grad_bf16x6."""
     rows, n_out = grad.shape
     k_in = x.shape[1]
     main = rows // 64 * 64
-    if main == 0 or not x6_wgrad_ok(main, n_out, k_in):
+    if main > 0 and first_wgrad_ok(main, n_out, k_in):
+        fn = first_weight_grad_x6
+    elif main > 0 and x6_wgrad_ok(main, n_out, k_in):
+        fn = weight_grad_x6
+    else:
         return torch.mm(grad.t(), x, out=out)
-    dw = weight_grad_x6(grad[:main], x[:main], out=out)
+    dw = fn(grad[:main], x[:main], out=out)
     if main < rows:
         dw = dw.addmm_(grad[main:].t(), x[main:])
     return dw

@@ -8,7 +8,8 @@ import pytest
 import torch
 
 from vss_amd import _native as N
-from vss_amd.update import (linear_tanh, linear_tanh_backward, linear_tanh_backward_mixed, linear_tanh_backward_x6,
+from vss_amd.update import (first_weight_grad_x6, first_wgrad_ok, linear_tanh, linear_tanh_backward,
+                            linear_tanh_backward_mixed, linear_tanh_backward_x6,
                             linear_tanh_mixed, linear_tanh_out_mixed, linear_tanh_out_x6, linear_tanh_x6,
                             weight_grad_mixed, weight_grad_x6, x6_ok, x6_wgrad_ok)
 
@@ -18,6 +19,15 @@ def test_x6_shape_predicates_cpu():
     assert not x6_ok(200, 512, 256) and not x6_ok(256, 52, 256) and not x6_ok(256, 512, 100)
     assert x6_wgrad_ok(64, 256, 128) and x6_wgrad_ok(2097152, 512, 512)
     assert not x6_wgrad_ok(100, 256, 128) and not x6_wgrad_ok(64, 128, 128) and not x6_wgrad_ok(64, 256, 52)
+
+
+def test_first_wgrad_shape_predicate_cpu():
+    """The first layer's weight gradient (nn.Linear(52, 256)): n_out 256, k_in <= 64 and % 4, rows % 64."""
+    assert first_wgrad_ok(2097152, 256, 52) and first_wgrad_ok(64, 256, 64) and first_wgrad_ok(131008, 256, 4)
+    assert not first_wgrad_ok(100, 256, 52) and not first_wgrad_ok(64, 512, 52) and not first_wgrad_ok(64, 256, 68)
+    assert not first_wgrad_ok(64, 256, 50)
+    with pytest.raises(ValueError):
+        first_weight_grad_x6(torch.zeros(64, 256), torch.zeros(64, 52))
 
 
 def test_x6_refuses_cpu_tensors():
@@ -87,6 +97,61 @@ def test_x6_weight_grad_error_at_most_fp32_gpu(rows, n_out, k_in):
     e6 = _rel(weight_grad_x6(gz, x), ref)
     et = _rel(gz.t().mm(x), ref)
     assert e6[0] < 4e-6 and e6[1] < 1.25 * et[1] + 1e-8, (e6, et)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k_in", [52, 4, 64, 36])
+@pytest.mark.parametrize("rows", [64, 8192, 131008, 2097152])
+def test_x6_first_layer_weight_grad_error_at_most_fp32_gpu(rows, k_in):
+    """The first layer's dW = g^T x (g (rows, 256), x (rows, k_in): the observations, 52 wide in the
+    Agent) on vss_first_weight_grad_bf16x6: error vs fp64 no larger than torch's fp32 mm (x 1.25), and
+    two calls give the same bits (fixed-order parts)."""
+    g = torch.Generator(device="cuda").manual_seed(rows + k_in)
+    gz = torch.randn(rows, 256, device="cuda", generator=g) * 1e-3
+    x = torch.randn(rows, k_in, device="cuda", generator=g) * 2.0
+    ref = gz.double().t() @ x.double()
+    got = first_weight_grad_x6(gz, x)
+    assert got.shape == (256, k_in)
+    e6 = _rel(got, ref)
+    et = _rel(gz.t().mm(x), ref)
+    assert e6[0] < 4e-6 and e6[1] < 1.25 * et[1] + 1e-8, (e6, et)
+    assert torch.equal(got, first_weight_grad_x6(gz, x))
+
+
+@pytest.mark.gpu
+def test_x6_first_layer_weight_grad_exact_and_per_product_gpu():
+    """Integer operands with exact fp32 sums give the exact dW; one nonzero row (an outer product of
+    full 24-bit values) is within 2^-22 |a b| of each product; a strided minibatch view (rows of a
+    larger observation buffer) gives the contiguous copy's bits."""
+    g = torch.Generator(device="cuda").manual_seed(3)
+    rows = 4096
+    gi = torch.randint(-100, 101, (rows, 256), device="cuda", generator=g).float()
+    xi = torch.randint(-300, 301, (rows, 52), device="cuda", generator=g).float()
+    assert torch.equal(first_weight_grad_x6(gi, xi).double(), gi.double().t() @ xi.double())
+    gz = torch.zeros(128, 256, device="cuda")
+    x = torch.zeros(128, 52, device="cuda")
+    gz[77] = torch.randn(256, device="cuda", generator=g) * 3.7
+    x[77] = torch.randn(52, device="cuda", generator=g) * 0.31
+    ref = gz[77].double()[:, None] * x[77].double()[None, :]
+    rel = ((first_weight_grad_x6(gz, x).double() - ref).abs() / ref.abs().clamp_min(1e-300)).max()
+    assert float(rel) <= 2 ** -22, float(rel)
+    big = torch.randn(2 * rows, 52, device="cuda", generator=g)
+    gz = torch.randn(rows, 256, device="cuda", generator=g)
+    assert torch.equal(first_weight_grad_x6(gz, big[::2]), first_weight_grad_x6(gz, big[::2].contiguous()))
+
+
+@pytest.mark.gpu
+def test_x6_first_layer_weight_grad_refusals_gpu():
+    lib = N.load()
+    buf = torch.zeros(1 << 20, device="cuda")
+    p, s = buf.data_ptr(), N.stream_of(buf.device)
+    assert lib.vss_first_weight_grad_chunks_bf16x6(100, 256, 52) == -1  # rows % 64
+    assert lib.vss_first_weight_grad_chunks_bf16x6(64, 512, 52) == -1   # n_out != 256
+    assert lib.vss_first_weight_grad_chunks_bf16x6(64, 256, 68) == -1   # k_in > 64
+    assert lib.vss_first_weight_grad_chunks_bf16x6(64, 256, 50) == -1   # k_in % 4
+    assert lib.vss_first_weight_grad_chunks_bf16x6(2097152, 256, 52) == 256
+    assert lib.vss_first_weight_grad_bf16x6(s, 64, 256, 52, p + 4, p, p) != 0  # misaligned grad
+    assert lib.vss_first_weight_grad_bf16x6(s, 64, 256, 52, p, p, None) != 0
 
 
 @pytest.mark.gpu

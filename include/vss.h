@@ -407,6 +407,33 @@ int vss_ppo_loss(void* stream, int64_t rows, int64_t rows_pad, int32_t n_act, co
                  float* grad_logstd, float* loss_out, float* stats_out, float* partial);
 
 /* ---------------------------------------------------------------------------------------------
+ * The update's gradient bookkeeping on flat buffers (csrc/vss_optim.hip; ppo_continuous_action_isaacgym.py
+ * FlatParams / FlatGrads / FlatAdam).  Replaces, per minibatch, nn.utils.clip_grad_norm_ (ppo…:353)
+ * and optim.Adam(eps=1e-5).step() (ppo…:166,354) -- torch's per-tensor norm chain and multi-tensor
+ * Adam -- with two launches, and the split GEMMs' torch.sum reductions with one launch per backward.
+ *
+ * vss_grad_sq_partials: partial[b] = sum of grad[i]^2 over block b's chunk, b < count =
+ *   vss_grad_sq_partials_count(n) (<= 1024; -1 for n <= 0); fixed order (deterministic).
+ * vss_adam_step_clipped: norm = sqrt(sum of the nparts partials); with max_norm > 0 the gradients are
+ *   scaled in place by min(1, max_norm / (norm + 1e-6)) (clip_grad_norm_); then Adam's step `step`
+ *   (>= 1, the count after this step) with torch's fused-Adam arithmetic: m = b1 m + (1 - b1) g,
+ *   v = b2 v + (1 - b2) g^2, p -= lr / (1 - b1^step) * m / (sqrt(v) / sqrt(1 - b2^step) + eps).
+ *   norm_out (1 float, may be NULL) receives the pre-clip norm.  All buffers n fp32 elements.
+ * vss_sum_parts: `count` (1..16) jobs; job q: dst[r * dst_ld + c] = sum over s = 0 .. parts - 1 of
+ *   src[s * part_stride + r * src_ld + c], r < rows, c < cols, in a fixed order (parts s = w + 4 (u + 8 i)
+ *   into running sum (w, u), then those sums in a fixed tree: deterministic).  Host arrays of count
+ *   entries; device buffers; src parts must not overlap dst.
+ * ------------------------------------------------------------------------------------------- */
+int64_t vss_grad_sq_partials_count(int64_t n);
+int vss_grad_sq_partials(void* stream, int64_t n, const float* grad, float* partial);
+int vss_adam_step_clipped(void* stream, int64_t n, int32_t nparts, const float* partial, float max_norm, float lr,
+                          float beta1, float beta2, float eps, int64_t step, float* grad, float* param, float* exp_avg,
+                          float* exp_avg_sq, float* norm_out);
+int vss_sum_parts(void* stream, int32_t count, const float* const* src, float* const* dst, const int64_t* parts,
+                  const int64_t* part_stride, const int64_t* rows, const int64_t* cols, const int64_t* src_ld,
+                  const int64_t* dst_ld);
+
+/* ---------------------------------------------------------------------------------------------
  * Episode statistics: RecordEpisodeStatisticsTorch.step (envs/wrappers.py:66-87)
  * for `rows` learner rows in one launch, in the reference's order:
  *   ep_returns += rews; ep_lengths += 1; returned_returns = ep_returns; returned_lengths =

@@ -58,7 +58,7 @@ from envs._gym import Box, ObservationWrapper  # noqa: E402
 from vss_amd.loss import ppo_loss  # noqa: E402
 from vss_amd.update import (first_wgrad_ok, gemm_shape_ok, linear_tanh, linear_tanh_backward, linear_tanh_backward_mixed,  # noqa: E402
                             linear_tanh_mixed, linear_tanh_out, linear_tanh_out_mixed, linear_tanh_out_ok,
-                            output_backward, output_backward_ok, weight_grad_mixed, weight_planes,
+                            output_backward, output_backward_ok, sum_parts, weight_grad_mixed, weight_planes,
                             x6_ok)
 
 
@@ -234,6 +234,9 @@ class _TanhMLP(torch.autograd.Function):
         hs, ws = saved[:n], saved[n:]  # hs[l] = input of layer l (hs[0] = x), ws[l] = its weight
         grads = [None] * (2 * n)
         dst = [_grad_dst(p) if gout.is_cuda else None for p in ctx.params]
+        # the split kernels' partial sums (weight gradients over row parts, bias column sums) reduced for
+        # the whole MLP in one launch at the end (sum_parts) when they go straight into FlatGrads
+        defer = [] if gout.is_cuda and all(d is not None for d in dst) else None
         gz = gout.contiguous()  # pre-activation gradient of the current layer
         gb = torch.sum(gz, 0, out=dst[2 * n - 1])
         for layer in reversed(range(n)):
@@ -242,13 +245,13 @@ class _TanhMLP(torch.autograd.Function):
                 # layer below in one streaming pass over that layer's output (vss_output_backward)
                 grads[2 * layer + 1] = gb
                 gz, gb, grads[2 * layer] = output_backward(gz, ws[layer], hs[layer], out_db=dst[2 * layer - 1],
-                                                           out_dw=dst[2 * layer])
+                                                           out_dw=dst[2 * layer], defer=defer)
                 continue
             x6 = gz.is_cuda and UPDATE_GEMM == "x6"
             if x6 and ((hs[layer].shape[1] % 128 == 0 and gz.shape[1] % 256 == 0) or
                        (layer == 0 and first_wgrad_ok(256, gz.shape[1], hs[0].shape[1]))):
                 # the hidden layers' and the first layer's weight gradients on the x6 kernels
-                grads[2 * layer] = weight_grad_mixed(gz, hs[layer], out=dst[2 * layer])
+                grads[2 * layer] = weight_grad_mixed(gz, hs[layer], out=dst[2 * layer], defer=defer)
             else:
                 grads[2 * layer] = _split_k_wgrad(gz, hs[layer], out=dst[2 * layer])
             grads[2 * layer + 1] = gb
@@ -262,11 +265,14 @@ class _TanhMLP(torch.autograd.Function):
                 gz, w = nn.functional.pad(gz, (0, pad)), nn.functional.pad(w, (0, 0, 0, pad))
             if x6:
                 gz, gb = linear_tanh_backward_mixed(gz, w, hs[layer], out_db=dst[2 * layer - 1],
-                                                    planes=ctx.planes_b.get(layer) if layer < n - 1 else None)
+                                                    planes=ctx.planes_b.get(layer) if layer < n - 1 else None,
+                                                    defer=defer)
             else:
                 gz, gb = linear_tanh_backward(gz, w, hs[layer])
                 if dst[2 * layer - 1] is not None:
                     gb = dst[2 * layer - 1].copy_(gb)
+        if defer:
+            sum_parts(defer)
         gx = gz.mm(ws[0]) if ctx.needs_input_grad[0] else None
         # the gradients already written into their parameters' .grad are not handed to autograd
         # (whose AccumulateGrad would add them to themselves)
@@ -359,17 +365,32 @@ def _grad_dst(p: torch.Tensor):
 class FlatGrads:
     """All parameter gradients as views of ONE contiguous fp32 buffer, so the data-parallel
     exchange is a single all-reduce (4.3 MB for the SA agent) with no pack/unpack copies.  The MLPs'
-    backward (_TanhMLP) writes their gradients straight into these views (_grad_dst)."""
+    backward (_TanhMLP) writes their gradients straight into these views (_grad_dst).  With
+    flat_params the parameters themselves become views of one buffer as well (same order), which
+    FlatAdam steps in one launch."""
 
-    def __init__(self, module: nn.Module):
+    ALIGN = 64  # floats: every tensor starts 256-B aligned (the HIP entries take 16-B aligned buffers)
+
+    def __init__(self, module: nn.Module, flat_params: bool = False):
         self.params = [p for p in module.parameters() if p.requires_grad]
-        total = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(total, device=self.params[0].device, dtype=torch.float32)
-        off = 0
+        offs, off = [], 0
         for p in self.params:
-            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            offs.append(off)
+            off = -(-(off + p.numel()) // self.ALIGN) * self.ALIGN
+        dev = self.params[0].device
+        # the gaps between tensors stay zero in both buffers (zero gradients leave them unchanged)
+        self.flat = torch.zeros(off, device=dev, dtype=torch.float32)
+        self.flat_p = torch.zeros(off, device=dev, dtype=torch.float32) if flat_params else None
+        self.optimizer = None  # a FlatAdam stepping these buffers (clip_norm_ then defers to it)
+        for p, o in zip(self.params, offs):
+            p.grad = self.flat[o:o + p.numel()].view_as(p)
             p._vss_flat_grad = True
-            off += p.numel()
+            if flat_params:
+                if p.dtype != torch.float32:
+                    raise ValueError("flat_params: fp32 parameters only")
+                view = self.flat_p[o:o + p.numel()].view_as(p)
+                view.copy_(p.detach())
+                p.data = view
 
     def zero(self):
         self.flat.zero_()
@@ -391,10 +412,63 @@ class FlatGrads:
     def clip_norm_(self, max_norm: float) -> torch.Tensor:
         """nn.utils.clip_grad_norm_(agent.parameters(), max_norm) (ppo…:353) on the flat buffer: the L2
         norm of all the gradients (one reduction instead of one per tensor and a norm of the norms), the
-        same coefficient max_norm / (norm + 1e-6) clamped to 1, one in-place scale.  Returns the norm."""
+        same coefficient max_norm / (norm + 1e-6) clamped to 1, one in-place scale.  Returns the norm.
+        With a FlatAdam attached the scale is applied inside its next step() (the norm's partial sums are
+        taken here, vss_grad_sq_partials; the returned tensor holds the norm once that step has run)."""
+        if self.optimizer is not None:
+            return self.optimizer.defer_clip(max_norm)
         total = torch.linalg.vector_norm(self.flat)
         self.flat.mul_(torch.clamp(max_norm / (total + 1e-6), max=1.0))
         return total
+
+
+class FlatAdam(torch.optim.Optimizer):
+    """optim.Adam(agent.parameters(), lr, eps=1e-5) (ppo…:166, step at ppo…:354) over FlatGrads' flat
+    parameter and gradient buffers: one launch (vss_adam_step_clipped) per step, which also applies the
+    clip_grad_norm_ (ppo…:353) requested through FlatGrads.clip_norm_ just before -- instead of torch's
+    norm chain and multi-tensor Adam (~8 launches, ~130 us per minibatch at the reference's 4,095 envs).
+    Same update rule, in torch's fused-Adam arithmetic (tests/test_ppo.py); param_groups[0]["lr"] is read
+    at every step, so --anneal-lr / --adaptative-lr act on it as on torch's Adam."""
+
+    def __init__(self, flat: FlatGrads, lr: float, betas=(0.9, 0.999), eps: float = 1e-5):
+        if flat.flat_p is None or not flat.flat.is_cuda:
+            raise ValueError("FlatAdam: a FlatGrads with flat_params=True on a ROCm device")
+        super().__init__(flat.params, dict(lr=lr, betas=betas, eps=eps))
+        from vss_amd import _native as N
+        self._N = N
+        self.flat = flat
+        flat.optimizer = self
+        n = flat.flat.numel()
+        self.exp_avg = torch.zeros_like(flat.flat_p)
+        self.exp_avg_sq = torch.zeros_like(flat.flat_p)
+        self.steps = 0
+        self.nparts = int(N.load().vss_grad_sq_partials_count(n))
+        self.partial = torch.zeros(self.nparts, device=flat.flat.device)
+        self.norm = torch.zeros(1, device=flat.flat.device)
+        self._max_norm = 0.0
+
+    def defer_clip(self, max_norm: float) -> torch.Tensor:
+        N = self._N
+        N.check(N.load().vss_grad_sq_partials(N.stream_of(self.flat.flat.device), self.flat.flat.numel(),
+                                              self.flat.flat.data_ptr(), self.partial.data_ptr()),
+                "vss_grad_sq_partials")
+        self._max_norm = float(max_norm)
+        return self.norm
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        if closure is not None:
+            raise ValueError("FlatAdam.step: no closure")
+        N = self._N
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        self.steps += 1
+        f = self.flat
+        N.check(N.load().vss_adam_step_clipped(
+            N.stream_of(f.flat.device), f.flat.numel(), self.nparts, self.partial.data_ptr(), self._max_norm,
+            float(g["lr"]), float(b1), float(b2), float(g["eps"]), self.steps, f.flat.data_ptr(), f.flat_p.data_ptr(),
+            self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.norm.data_ptr()), "vss_adam_step_clipped")
+        self._max_norm = 0.0  # a clip applies to the step right after it only
 
 
 class _NullWriter:
@@ -839,14 +913,17 @@ def train(args, on_update=None):
     assert isinstance(envs.single_action_space, Box), "only continuous action space is supported"
 
     agent = Agent(envs).to(device)
-    flat = FlatGrads(agent)
+    flat = FlatGrads(agent, flat_params=device.type == "cuda")
     fused = None
     if args.fused_policy and device.type == "cuda" and args.amp == "none":
         from vss_amd.policy import FusedPolicy
         fused = FusedPolicy(agent, seed=seed * 7919 + 17)
-    # torch's Adam (ppo…:166) -- on the GPU its fused implementation: one kernel per step instead of
-    # seven multi-tensor passes (~0.2 ms per minibatch at 4,095 envs), the same update rule
-    optimizer = optim.Adam(agent.parameters(), lr=args.learning_rate, eps=1e-5, fused=device.type == "cuda")
+    # torch's Adam (ppo…:166) -- on the GPU FlatAdam: the same update rule over the flat parameter and
+    # gradient buffers, with the gradient clip, in one launch per minibatch (vss_adam_step_clipped)
+    if device.type == "cuda":
+        optimizer = FlatAdam(flat, lr=args.learning_rate, eps=1e-5)
+    else:
+        optimizer = optim.Adam(agent.parameters(), lr=args.learning_rate, eps=1e-5)
     gen = torch.Generator(device=device).manual_seed(seed)
 
     T, E = args.num_steps, args.num_envs

@@ -23,7 +23,7 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "vss.h"
 # the sources the Makefile stamps into the library, in its order (csrc/Makefile STAMPED)
 STAMPED = (os.path.join(CSRC, "vss_step.hip"), os.path.join(CSRC, "vss_update.hip"),
            os.path.join(CSRC, "vss_policy.hip"), os.path.join(CSRC, "vss_gemm_x6.hip"),
-           os.path.join(CSRC, "vss_loss.hip"), HEADER,
+           os.path.join(CSRC, "vss_loss.hip"), os.path.join(CSRC, "vss_optim.hip"), HEADER,
            os.path.join(CSRC, "Makefile"))
 
 ABI_VERSION = 2
@@ -39,7 +39,8 @@ EXPORTED = ("vss_abi_version", "vss_source_hash", "vss_error_string", "vss_step"
             "vss_output_backward_chunks", "vss_output_backward", "vss_linear_tanh_bf16x6",
             "vss_linear_tanh_out_bf16x6", "vss_linear_tanh_backward_chunks_bf16x6", "vss_linear_tanh_backward_bf16x6",
             "vss_weight_grad_chunks_bf16x6", "vss_weight_grad_bf16x6", "vss_first_weight_grad_chunks_bf16x6",
-            "vss_first_weight_grad_bf16x6", "vss_weight_planes_bf16x6", "vss_ppo_loss_scratch_floats", "vss_ppo_loss")
+            "vss_first_weight_grad_bf16x6", "vss_weight_planes_bf16x6", "vss_ppo_loss_scratch_floats", "vss_ppo_loss",
+            "vss_grad_sq_partials_count", "vss_grad_sq_partials", "vss_adam_step_clipped", "vss_sum_parts")
 
 
 class VssParams(ctypes.Structure):
@@ -185,6 +186,14 @@ def load() -> ctypes.CDLL:
     L.vss_ppo_loss_scratch_floats.restype = i64
     L.vss_ppo_loss.argtypes = [P, i64, i64, i32] + [P] * 8 + [f32] * 5 + [i32] + [P] * 6
     L.vss_ppo_loss.restype = ctypes.c_int
+    L.vss_grad_sq_partials_count.argtypes = [i64]
+    L.vss_grad_sq_partials_count.restype = i64
+    L.vss_grad_sq_partials.argtypes = [P, i64, P, P]
+    L.vss_grad_sq_partials.restype = ctypes.c_int
+    L.vss_adam_step_clipped.argtypes = [P, i64, i32, P] + [f32] * 5 + [i64] + [P] * 5
+    L.vss_adam_step_clipped.restype = ctypes.c_int
+    L.vss_sum_parts.argtypes = [P, i32] + [P] * 8
+    L.vss_sum_parts.restype = ctypes.c_int
     if L.vss_abi_version() != ABI_VERSION:
         raise NativeError(f"libvss_amd ABI {L.vss_abi_version()} != expected {ABI_VERSION}")
     _lib = L

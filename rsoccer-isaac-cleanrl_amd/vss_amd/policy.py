@@ -15,7 +15,9 @@ of the update's GEMM kernels -- first layer on the fp32 MFMA kernel, the 256/512
 arithmetic on the bf16 matrix cores (csrc/vss_gemm_x6.hip, output layer folded into the last launch)
 -- and vss_policy_sample draws the actions from the actor means with the fused kernel's Philox
 stream: 0.93 ms instead of 1.21 ms for actor + critic at 65,536 rows (profiles/r03o_*).  Smaller
-batches keep the single fused launch.  VSS_ROLLOUT_POLICY=fused forces the fused kernel.
+batches keep the single fused launch.  VSS_ROLLOUT_POLICY=fused forces the fused kernel.  The chain's
+bf16 weight planes are made once per refresh(), like the fused kernel's packed weights: both evaluate
+the weights as of the last refresh().
 """
 from __future__ import annotations
 
@@ -25,7 +27,7 @@ import os
 import torch
 
 from . import _native as N
-from .update import linear_tanh_mixed, linear_tanh_out_mixed
+from .update import linear_tanh_mixed, linear_tanh_out_mixed, weight_planes, x6_ok
 
 CHAIN_MIN_ROWS = 16384
 ROLLOUT_POLICY = os.environ.get("VSS_ROLLOUT_POLICY", "chain")
@@ -65,18 +67,30 @@ class FusedPolicy:
 
     @torch.no_grad()
     def refresh(self):
-        """Re-pack the current actor / critic weights (call after optimizer.step())."""
+        """Re-pack the current actor / critic weights (call after optimizer.step()): the fused kernel's
+        packed weights and the GEMM chain's bf16 weight planes (one vss_weight_planes_bf16x6 launch for
+        both MLPs' hidden layers, instead of a split launch per layer and rollout step)."""
         self._pack(self.agent.actor_mean, self.n_act, self._actor)
         self._pack(self.agent.critic, 1, self._critic)
+        self._planes = {}
+        if ROLLOUT_POLICY == "chain":
+            jobs = [(id(seq), i, m.weight.detach()) for seq in (self.agent.actor_mean, self.agent.critic)
+                    for i, m in enumerate(self._linears(seq)[1:-1], 1)
+                    if m.weight.dtype == torch.float32 and m.weight.is_contiguous()
+                    and x6_ok(256, m.in_features, m.out_features)]
+            if jobs:
+                planes = weight_planes([(w, False) for _, _, w in jobs])
+                self._planes = {(k, i): p for (k, i, _), p in zip(jobs, planes)}
 
     def _chain(self, seq, obs):
         """One MLP's output (rows, n_out) through the update's GEMM kernels (no autograd)."""
         lins = self._linears(seq)
         h = obs
-        for m in lins[:-2]:
-            h = linear_tanh_mixed(h, m.weight.detach(), m.bias.detach())
+        pl = self._planes
+        for i, m in enumerate(lins[:-2]):
+            h = linear_tanh_mixed(h, m.weight.detach(), m.bias.detach(), planes=pl.get((id(seq), i)))
         return linear_tanh_out_mixed(h, lins[-2].weight.detach(), lins[-2].bias.detach(), lins[-1].weight.detach(),
-                                     lins[-1].bias.detach())[1]
+                                     lins[-1].bias.detach(), planes=pl.get((id(seq), len(lins) - 2)))[1]
 
     def chain_active(self, rows: int) -> bool:
         """Whether a batch of `rows` observations is evaluated by the GEMM chain."""

@@ -68,6 +68,46 @@ def _out(out, shape, like):
     return out
 
 
+def _reduce_parts(parts: torch.Tensor, out: torch.Tensor | None, defer: list | None) -> torch.Tensor:
+    """The sum over dim 0 of a kernel's partial results, into `out` when given; with a `defer` list (and
+    an `out`) the reduction is queued there for ONE sum_parts launch later (the result is read only after
+    that launch: the update's gradients, read by the optimizer)."""
+    if defer is not None and out is not None and parts.is_cuda:
+        defer.append((parts, out))
+        return out
+    return torch.sum(parts, 0, out=out)
+
+
+def sum_parts(jobs) -> None:
+    """jobs = [(parts (S, ...) fp32, out (...) fp32)]: out = parts.sum(0) for all of them in one launch
+    per 16 jobs (vss_sum_parts; parts summed in order s = 0 .. S-1, deterministic).  `out` may be a
+    row-strided 2-D view; the last dim of both must be contiguous."""
+    jobs = list(jobs)
+    for q0 in range(0, len(jobs), 16):
+        chunk = jobs[q0:q0 + 16]
+        cols = {k: [] for k in ("src", "dst", "parts", "pstride", "rows", "cols", "sld", "dld")}
+        for parts, out in chunk:
+            p3 = parts.reshape(parts.shape[0], -1, parts.shape[-1]) if parts.dim() >= 2 else None
+            o2 = out.reshape(1, -1) if out.dim() == 1 else out
+            if p3 is None or parts.dtype != torch.float32 or out.dtype != torch.float32 or o2.dim() != 2 \
+                    or tuple(p3.shape[1:]) != tuple(o2.shape) or p3.stride(2) != 1 or o2.stride(1) != 1 \
+                    or not parts.is_cuda or out.device != parts.device:
+                raise ValueError(f"sum_parts: parts {tuple(parts.shape)} / out {tuple(out.shape)}")
+            cols["src"].append(p3.data_ptr())
+            cols["dst"].append(o2.data_ptr())
+            cols["parts"].append(p3.shape[0])
+            cols["pstride"].append(p3.stride(0))
+            cols["rows"].append(o2.shape[0])
+            cols["cols"].append(o2.shape[1])
+            cols["sld"].append(p3.stride(1) if o2.shape[0] > 1 else o2.shape[1])
+            cols["dld"].append(o2.stride(0) if o2.shape[0] > 1 else o2.shape[1])
+        c = len(chunk)
+        Pa, I64 = ctypes.c_void_p * c, ctypes.c_int64 * c
+        N.check(N.load().vss_sum_parts(N.stream_of(chunk[0][0].device), c, Pa(*cols["src"]), Pa(*cols["dst"]),
+                                       I64(*cols["parts"]), I64(*cols["pstride"]), I64(*cols["rows"]),
+                                       I64(*cols["cols"]), I64(*cols["sld"]), I64(*cols["dld"])), "vss_sum_parts")
+
+
 def linear_tanh(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """tanh(x @ w.T + b) for x (rows, k), w (n, k) (nn.Linear's weight), b (n,)."""
     if x.dim() != 2 or w.dim() != 2 or x.shape[1] != w.shape[1] or b.shape != (w.shape[0],):
@@ -151,7 +191,7 @@ def output_backward_ok(k_out: int, n: int) -> bool:
 
 
 def output_backward(g_out: torch.Tensor, w_out: torch.Tensor, y: torch.Tensor, out_db: torch.Tensor | None = None,
-                    out_dw: torch.Tensor | None = None):
+                    out_dw: torch.Tensor | None = None, defer: list | None = None):
     """Backward through the output nn.Linear (weight w_out (k_out, n)) into the tanh layer below it
     (output y (rows, n), also the output layer's input), g_out (rows, k_out) the output's gradient:
     gz = (g_out @ w_out) * (1 - y^2), db = gz.sum(0) and dw = g_out.T @ y (the output layer's weight
@@ -182,7 +222,7 @@ def output_backward(g_out: torch.Tensor, w_out: torch.Tensor, y: torch.Tensor, o
     N.check(lib.vss_output_backward(N.stream_of(y.device), rows, k_pad, n, g_pad.data_ptr(), w_t.data_ptr(),
                                     y.data_ptr(), gz.data_ptr(), bpart.data_ptr(), wpart.data_ptr()),
             "vss_output_backward")
-    return gz, torch.sum(bpart, 0, out=out_db), torch.sum(wpart[:, :k_out], 0, out=out_dw)
+    return gz, _reduce_parts(bpart, out_db, defer), _reduce_parts(wpart[:, :k_out], out_dw, defer)
 
 
 # ---- the same GEMMs in fp32 arithmetic on the bf16 matrix cores (csrc/vss_gemm_x6.hip) ----------------
@@ -290,7 +330,7 @@ def linear_tanh_out_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out:
 
 def linear_tanh_backward_x6(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.Tensor,
                             out: torch.Tensor | None = None, out_db: torch.Tensor | None = None,
-                            planes: torch.Tensor | None = None):
+                            planes: torch.Tensor | None = None, defer: list | None = None):
     """linear_tanh_backward on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_backward_bf16x6);
     planes: w_next's weight_planes() with transpose True, or None to transpose and split it in the call."""
     rows, k_next = gz_next.shape
@@ -310,10 +350,11 @@ def linear_tanh_backward_x6(gz_next: torch.Tensor, w_next: torch.Tensor, y: torc
                                                 wp, y.data_ptr(), gz.data_ptr(), partial.data_ptr(), pp),
             "vss_linear_tanh_backward_bf16x6")
     del keep  # the split and the GEMM are queued: the scratch may be reused from here on
-    return gz, torch.sum(partial, 0, out=out_db)
+    return gz, _reduce_parts(partial, out_db, defer)
 
 
-def weight_grad_x6(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def weight_grad_x6(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
+                   defer: list | None = None) -> torch.Tensor:
     """dW = grad.T @ x (a Linear layer's weight gradient, grad (rows, n_out), x (rows, k_in)) on the
     bf16 matrix cores with fp32 arithmetic, split over the rows (vss_weight_grad_bf16x6); the parts are
     reduced into `out` when given."""
@@ -326,7 +367,7 @@ def weight_grad_x6(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None
                         dtype=torch.float32)
     N.check(lib.vss_weight_grad_bf16x6(N.stream_of(x.device), rows, n_out, k_in, grad.data_ptr(), x.data_ptr(),
                                        parts.data_ptr()), "vss_weight_grad_bf16x6")
-    return torch.sum(parts, 0, out=out)
+    return _reduce_parts(parts, out, defer)
 
 
 def first_wgrad_ok(rows: int, n_out: int, k_in: int) -> bool:
@@ -335,7 +376,8 @@ def first_wgrad_ok(rows: int, n_out: int, k_in: int) -> bool:
     return rows > 0 and rows % 64 == 0 and n_out == 256 and 0 < k_in <= 64 and k_in % 4 == 0
 
 
-def first_weight_grad_x6(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def first_weight_grad_x6(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
+                         defer: list | None = None) -> torch.Tensor:
     """dW = grad.T @ x for the Agent's first layer (grad (rows, 256), x (rows, k_in <= 64): the
     observations) on the bf16 matrix cores with fp32 arithmetic, split over the rows
     (vss_first_weight_grad_bf16x6); the parts are reduced into `out` when given."""
@@ -348,7 +390,7 @@ def first_weight_grad_x6(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor 
                         dtype=torch.float32)
     N.check(lib.vss_first_weight_grad_bf16x6(N.stream_of(x.device), rows, n_out, k_in, grad.data_ptr(), x.data_ptr(),
                                              parts.data_ptr()), "vss_first_weight_grad_bf16x6")
-    return torch.sum(parts, 0, out=out)
+    return _reduce_parts(parts, out, defer)
 
 
 # ---- any row count: whole tiles on the bf16x6 kernels, the ragged rest on the fp32 ones --------------
@@ -388,9 +430,11 @@ def linear_tanh_out_mixed(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_o
 
 
 def linear_tanh_backward_mixed(gz_next: torch.Tensor, w_next: torch.Tensor, y: torch.Tensor,
-                               out_db: torch.Tensor | None = None, planes: torch.Tensor | None = None):
+                               out_db: torch.Tensor | None = None, planes: torch.Tensor | None = None,
+                               defer: list | None = None):
     """out_db: where to reduce the bias gradient into (the same tensor returned); planes: w_next's
-    weight_planes() with transpose True (None: split in the call)."""
+    weight_planes() with transpose True (None: split in the call); defer: queue the bias reduction
+    (_reduce_parts) when the rows are whole tiles."""
     rows, k_next = gz_next.shape
     n = y.shape[1]
     main = rows // 256 * 256
@@ -398,7 +442,8 @@ def linear_tanh_backward_mixed(gz_next: torch.Tensor, w_next: torch.Tensor, y: t
         gz, db = linear_tanh_backward(gz_next, w_next, y)
         return gz, (db if out_db is None else out_db.copy_(db))
     gz = torch.empty((rows, n), device=y.device, dtype=torch.float32)
-    _, db = linear_tanh_backward_x6(gz_next[:main], w_next, y[:main], out=gz[:main], out_db=out_db, planes=planes)
+    _, db = linear_tanh_backward_x6(gz_next[:main], w_next, y[:main], out=gz[:main], out_db=out_db, planes=planes,
+                                    defer=defer if main == rows else None)
     if main < rows:
         y_t = y[main:]
         gz_t = torch.mm(gz_next[main:], w_next, out=gz[main:]).mul_(1.0 - y_t * y_t)
@@ -406,7 +451,8 @@ def linear_tanh_backward_mixed(gz_next: torch.Tensor, w_next: torch.Tensor, y: t
     return gz, db
 
 
-def weight_grad_mixed(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def weight_grad_mixed(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
+                      defer: list | None = None) -> torch.Tensor:
     """out: where to reduce the weight gradient into (the same tensor returned).  The hidden layers'
     shapes on vss_weight_grad_bf16x6, the first layer's (x = the observations) on
     vss_first_weight_grad_bf16x6."""
@@ -419,7 +465,7 @@ def weight_grad_mixed(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | N
         fn = weight_grad_x6
     else:
         return torch.mm(grad.t(), x, out=out)
-    dw = fn(grad[:main], x[:main], out=out)
+    dw = fn(grad[:main], x[:main], out=out, defer=defer if main == rows else None)
     if main < rows:
         dw = dw.addmm_(grad[main:].t(), x[main:])
     return dw

@@ -81,6 +81,25 @@ def test_refresh_tracks_parameter_updates():
     torch.testing.assert_close(fused.get_value(obs), want, rtol=2e-5, atol=2e-6)
 
 
+def test_refresh_tracks_parameter_updates_on_the_chain_path():
+    """At rollout sizes (the GEMM chain) refresh() also renews the chain's x6 weight planes: after a
+    parameter change and refresh() the values follow the new weights."""
+    from vss_amd import policy as PM
+    agent = make_agent(2, 6)
+    fused = PM.FusedPolicy(agent)
+    rows = PM.CHAIN_MIN_ROWS
+    obs = torch.randn(rows, 52, device=DEV)
+    assert fused.chain_active(rows)
+    v0 = fused.get_value(obs)
+    with torch.no_grad():
+        for p in agent.parameters():
+            p.add_(0.01 * torch.randn_like(p))
+        want = agent.get_value(obs)
+    assert not torch.allclose(v0, want, rtol=1e-4, atol=1e-5)
+    fused.refresh()
+    torch.testing.assert_close(fused.get_value(obs), want, rtol=2e-5, atol=2e-6)
+
+
 def test_masked_terminal_values_write_only_masked_rows():
     from vss_amd.policy import FusedPolicy
     agent = make_agent(2, 5)

@@ -64,17 +64,21 @@ def test_gae_known_answers():
 
 
 def test_flat_grads_are_views():
+    """Every parameter's .grad is a view of the one flat buffer (1,079,045 gradients of the SA agent, each
+    tensor starting 256-B aligned: 1,079,232 floats with the gaps, which stay zero)."""
     agent = make_agent(2)
     flat = P.FlatGrads(agent)
-    assert flat.flat.numel() == 1079045
+    assert sum(p.numel() for p in agent.parameters()) == 1079045 and flat.flat.numel() == 1079232
     loss = agent.get_action_and_value(torch.randn(8, 52))[3].sum()
     flat.zero()
     loss.backward()
     assert flat.flat.abs().sum() > 0
-    off = 0
+    off, mask = 0, torch.zeros(flat.flat.numel(), dtype=torch.bool)
     for p in agent.parameters():
         assert p.grad.data_ptr() == flat.flat[off:off + p.numel()].data_ptr()
-        off += p.numel()
+        mask[off:off + p.numel()] = True
+        off = -(-(off + p.numel()) // 64) * 64
+    assert torch.count_nonzero(flat.flat[~mask]) == 0
 
 
 @pytest.mark.gpu
@@ -589,30 +593,85 @@ def test_importing_the_train_module_changes_no_environment_variable():
 
 
 @pytest.mark.gpu
-def test_fused_adam_and_flat_clip_match_reference_optimizer_step_gpu():
-    """train() steps torch's fused Adam on the GPU and clips the flat gradient buffer in one reduction;
-    the reference steps torch's default (multi-tensor) Adam after clip_grad_norm_ over the parameters
-    (ppo…:166, 353).  Same update rule: one update of 2 epochs x 2 minibatches ends within fp32
-    rounding of the reference's (1e-6 relative, 1e-7 absolute)."""
+@pytest.mark.parametrize("product", ["fused_adam", "flat_adam"])
+def test_product_optimizer_step_matches_reference_optimizer_step_gpu(product):
+    """train() steps FlatAdam on the GPU (flat parameters and gradients, the clip folded into the step:
+    vss_grad_sq_partials + vss_adam_step_clipped); round 4 stepped torch's fused Adam after one flat-norm
+    clip.  The reference steps torch's default (multi-tensor) Adam after clip_grad_norm_ over the
+    parameters (ppo…:166, 353).  Same update rule: one update of 2 epochs x 2 minibatches (and, for
+    FlatAdam, a second update with a lower lr set through param_groups, as --anneal-lr does) ends within
+    fp32 rounding of the reference's (1e-6 relative, 1e-7 absolute)."""
     args = _args(norm_adv=True, clip_vloss=False)
+    args.max_grad_norm = 0.05  # small enough that the clip scales every minibatch's gradients
     obs, act, logp, adv, ret, val = [t.cuda() for t in _synthetic_batch(5, 32768)]
     res = []
-    for fused in (False, True):
+    for mine in (False, True):
         agent = make_agent(2).cuda()
-        flat = P.FlatGrads(agent)
-        opt = torch.optim.Adam(agent.parameters(), lr=1e-3, eps=1e-5, fused=fused)
+        if mine and product == "flat_adam":
+            flat = P.FlatGrads(agent, flat_params=True)
+            opt = P.FlatAdam(flat, lr=1e-3, eps=1e-5)
+        else:
+            flat = P.FlatGrads(agent)
+            opt = torch.optim.Adam(agent.parameters(), lr=1e-3, eps=1e-5, fused=mine)
         gen = torch.Generator(device="cuda").manual_seed(7)
-        if fused:
-            P.ppo_update(agent, opt, flat, args, obs, logp, act, adv, ret, val, gen=gen)
-        else:  # the reference's clip over the parameters
-            orig = P.FlatGrads.clip_norm_
-            try:
-                P.FlatGrads.clip_norm_ = lambda self, m: torch.nn.utils.clip_grad_norm_(agent.parameters(), m)
+        for upd in range(2 if product == "flat_adam" else 1):
+            opt.param_groups[0]["lr"] = 1e-3 / (1 + upd)
+            if mine:
                 P.ppo_update(agent, opt, flat, args, obs, logp, act, adv, ret, val, gen=gen)
-            finally:
-                P.FlatGrads.clip_norm_ = orig
+            else:  # the reference's clip over the parameters
+                orig = P.FlatGrads.clip_norm_
+                try:
+                    P.FlatGrads.clip_norm_ = lambda self, m: torch.nn.utils.clip_grad_norm_(agent.parameters(), m)
+                    P.ppo_update(agent, opt, flat, args, obs, logp, act, adv, ret, val, gen=gen)
+                finally:
+                    P.FlatGrads.clip_norm_ = orig
         res.append(torch.cat([p.detach().reshape(-1) for p in agent.parameters()]))
     torch.testing.assert_close(res[1], res[0], rtol=1e-6, atol=1e-7)
+
+
+def test_flat_params_are_views_of_one_buffer_cpu():
+    """FlatGrads(flat_params=True): every parameter becomes a view of one buffer (same values, same
+    Parameter objects, the reference's state-dict keys), in parameter order, each 256-B aligned (the
+    critic's output bias has 1 element: the actor's weights would otherwise start misaligned)."""
+    agent = make_agent(2)
+    before = {k: v.clone() for k, v in agent.state_dict().items()}
+    ids = [id(p) for p in agent.parameters()]
+    flat = P.FlatGrads(agent, flat_params=True)
+    assert [id(p) for p in agent.parameters()] == ids
+    after = agent.state_dict()
+    assert list(after) == list(before) and all(torch.equal(after[k], before[k]) for k in before)
+    off = 0
+    for p in agent.parameters():
+        assert p.data_ptr() == flat.flat_p.data_ptr() + 4 * off and p.grad.data_ptr() == flat.flat.data_ptr() + 4 * off
+        assert p.data_ptr() % 256 == flat.flat_p.data_ptr() % 256  # every tensor 256-B aligned in the buffer
+        off = -(-(off + p.numel()) // 64) * 64
+    assert off == flat.flat_p.numel()
+    with pytest.raises(ValueError):
+        P.FlatAdam(flat, lr=1e-3)  # a CPU buffer: FlatAdam is the ROCm path
+
+
+@pytest.mark.gpu
+def test_sum_parts_matches_torch_sum_gpu():
+    """vss_sum_parts (one launch for many part reductions): 3-D parts into a contiguous and a row-strided
+    out, 2-D parts into a 1-D out (also 256 parts of 512 columns: the bias column sums' shape); equal to the
+    parts summed one after another within fp32 summation-order rounding, and the same bits on a repeat."""
+    from vss_amd.update import sum_parts
+    g = torch.Generator(device="cuda").manual_seed(3)
+    a = torch.randn(32, 512, 256, device="cuda", generator=g)
+    b = torch.randn(7, 4, 256, device="cuda", generator=g)[:, :2]  # strided parts (a padded slice)
+    c = torch.randn(5, 300, device="cuda", generator=g)
+    d = torch.randn(256, 512, device="cuda", generator=g)
+    outs = [torch.empty(512, 256, device="cuda"), torch.full((2, 300), 7.0, device="cuda")[:, :256],
+            torch.empty(300, device="cuda"), torch.empty(512, device="cuda")]
+    jobs = [(a, outs[0]), (b, outs[1]), (c, outs[2]), (d, outs[3])]
+    sum_parts(jobs)
+    first = [o.clone() for o in outs]
+    sum_parts(jobs)
+    for (parts, out), f in zip(jobs, first):
+        assert torch.equal(out, f)
+        want = parts.double().sum(0)
+        scale = float(parts.double().abs().sum(0).max())
+        assert float((out.double() - want).abs().max()) <= 2e-7 * scale
 
 
 @pytest.mark.gpu

@@ -235,8 +235,9 @@ class _TanhMLP(torch.autograd.Function):
         grads = [None] * (2 * n)
         dst = [_grad_dst(p) if gout.is_cuda else None for p in ctx.params]
         # the split kernels' partial sums (weight gradients over row parts, bias column sums) reduced for
-        # the whole MLP in one launch at the end (sum_parts) when they go straight into FlatGrads
-        defer = [] if gout.is_cuda and all(d is not None for d in dst) else None
+        # the whole MLP in one launch at the end (sum_parts), whether they go straight into FlatGrads or
+        # back to autograd (the same kernels in the same order: the same bits either way)
+        defer = [] if gout.is_cuda else None
         gz = gout.contiguous()  # pre-activation gradient of the current layer
         gb = torch.sum(gz, 0, out=dst[2 * n - 1])
         for layer in reversed(range(n)):
@@ -447,7 +448,12 @@ class FlatAdam(torch.optim.Optimizer):
         self.norm = torch.zeros(1, device=flat.flat.device)
         self._max_norm = 0.0
 
+    def zero_grad(self, set_to_none: bool = True):
+        """Zero the flat gradient buffer (the .grad tensors are views of it and stay in place)."""
+        self.flat.zero()
+
     def defer_clip(self, max_norm: float) -> torch.Tensor:
+        """Take the norm's partial sums of the current gradients now; the next step() applies the clip."""
         N = self._N
         N.check(N.load().vss_grad_sq_partials(N.stream_of(self.flat.flat.device), self.flat.flat.numel(),
                                               self.flat.flat.data_ptr(), self.partial.data_ptr()),

@@ -69,10 +69,12 @@ def _out(out, shape, like):
 
 
 def _reduce_parts(parts: torch.Tensor, out: torch.Tensor | None, defer: list | None) -> torch.Tensor:
-    """The sum over dim 0 of a kernel's partial results, into `out` when given; with a `defer` list (and
-    an `out`) the reduction is queued there for ONE sum_parts launch later (the result is read only after
-    that launch: the update's gradients, read by the optimizer)."""
-    if defer is not None and out is not None and parts.is_cuda:
+    """The sum over dim 0 of a kernel's partial results, into `out` when given; with a `defer` list the
+    reduction is queued there for ONE sum_parts launch later (into `out`, or a new tensor returned now and
+    filled by that launch: the caller reads it only after running the list)."""
+    if defer is not None and parts.is_cuda:
+        if out is None:
+            out = torch.empty(parts.shape[1:], device=parts.device, dtype=torch.float32)
         defer.append((parts, out))
         return out
     return torch.sum(parts, 0, out=out)

@@ -651,6 +651,19 @@ def test_flat_params_are_views_of_one_buffer_cpu():
 
 
 @pytest.mark.gpu
+def test_flat_adam_zero_grad_keeps_the_flat_views_gpu():
+    """optimizer.zero_grad() (torch's default would set every .grad to None and break the views the MLPs'
+    backward writes into) zeroes the flat buffer instead."""
+    agent = make_agent(2).cuda()
+    flat = P.FlatGrads(agent, flat_params=True)
+    opt = P.FlatAdam(flat, lr=1e-3)
+    flat.flat.fill_(1.0)
+    opt.zero_grad()
+    assert all(p.grad is not None and p.grad.data_ptr() >= flat.flat.data_ptr() for p in agent.parameters())
+    assert float(flat.flat.abs().sum()) == 0.0
+
+
+@pytest.mark.gpu
 def test_sum_parts_matches_torch_sum_gpu():
     """vss_sum_parts (one launch for many part reductions): 3-D parts into a contiguous and a row-strided
     out, 2-D parts into a 1-D out (also 256 parts of 512 columns: the bias column sums' shape); equal to the

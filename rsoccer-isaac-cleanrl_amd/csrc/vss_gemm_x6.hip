@@ -645,21 +645,25 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
 
 // ---- the first layer's weight gradient: dW (256, k_in <= 64) = grad^T x over all rows ----------------
 // The Agent's first Linear (52 -> 256, ppo…:131,142) under loss.backward() (ppo…:352): grad (rows, 256)
-// is the first tanh layer's pre-activation gradient, x (rows, k_in) the observations.  A block of 4 waves
-// takes a contiguous range of K tiles (32 rows each) and accumulates the whole (256, 64) tile, wave w the
-// features 64 w .. 64 w + 63 (4 x 4 MFMA tiles); the grid's parts are summed by the caller.  The bytes are
-// the operands once (HBM-bound: 1,024 + 4 k_in B per row); the six products keep it well under that roof.
+// is the first tanh layer's pre-activation gradient, x (rows, k_in) the observations.  A block of 8 waves
+// (two per SIMD, so one wave's staging runs beside the other's MFMAs) takes a contiguous range of K tiles
+// (32 rows each) and accumulates the whole (256, 64) tile, wave w the features 64 (w & 3) .. + 63 and the
+// columns 32 (w >> 2) .. + 31 (4 x 2 MFMA tiles); the grid's parts are summed by the caller.  The bytes
+// are the operands once (HBM-bound: 1,024 + 4 k_in B per row); the six products keep it under that roof.
+// (A first version with 4 waves, one per SIMD, ran no faster than hipBLASLt's split-K GEMM: 602 us at
+// 2,097,152 rows, profiles/r05h_bench_kernel_stats_by_grid.csv -- each SIMD staged and computed in turn.)
 //   grad: the K tile's 32 x 256 floats (32 KB contiguous) staged as ST_KROW into a KImg<256> image;
 //   x:    its 32 x k_in floats (contiguous, k_in % 4 == 0) as 16-B chunks of 4 columns, in a 4 KB-per-plane
 //         image of 16 LDS rows x 128 features: contraction row r sits at LDS row r & 15, feature
 //         c + 64 (r >> 4), the 16-B chunks XOR-swizzled by kswz(row) as in KImg -- so the transposed
 //         fragment reads are those of KImg (16 distinct 16-B slots per 32-lane half).  Columns k_in .. 63
 //         stay zero (written once).
-constexpr int FW_THREADS = 256, FW_N = 256, FW_KMAX = 64;
+constexpr int FW_THREADS = 512, FW_N = 256, FW_KMAX = 64;
 constexpr int FW_XPS = 16 * 256;                         // x image bytes per plane
 constexpr int FW_GPS = KImg<FW_N>::PS;                   // grad image bytes per plane
 constexpr int FW_BUF = 3 * FW_GPS + 3 * FW_XPS;          // 60 KB
-constexpr int FW_NX = (32 * FW_KMAX / 4) / FW_THREADS;   // x chunks per thread (2)
+constexpr int FW_NX = (32 * FW_KMAX / 4 + FW_THREADS - 1) / FW_THREADS;  // x chunks per thread (1)
+constexpr int FW_NG = 32 * FW_N / 8 / FW_THREADS;         // grad (row, 8-feature group) pairs per thread (2)
 
 // byte offset in one x plane of contraction row r, feature column c (c % 4 == 0): the 8-B piece of c .. c + 3
 __device__ __forceinline__ int fw_xoff(int r, int c) {
@@ -681,7 +685,7 @@ __global__ __launch_bounds__(FW_THREADS, 1) void first_wgrad_kernel(int64_t kpai
     *reinterpret_cast<u32x4*>(lds + buf * FW_BUF + 3 * FW_GPS + 16 * o) = (u32x4){0u, 0u, 0u, 0u};
   }
   struct St {
-    u32x4 g[4][2];
+    u32x4 g[FW_NG][2];
     u32x4 x[FW_NX];
   };
   int64_t f_kt = 0;
@@ -690,7 +694,7 @@ __global__ __launch_bounds__(FW_THREADS, 1) void first_wgrad_kernel(int64_t kpai
     ++f_kt;
     const float* gsrc = grad + kt * 32 * FW_N;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < FW_NG; ++u) {
       const int pr = tid + FW_THREADS * u, row = pr >> 5, cc = pr & 31;  // 8 consecutive features of one row
       s.g[u][0] = *reinterpret_cast<const u32x4*>(gsrc + row * FW_N + 8 * cc);
       s.g[u][1] = *reinterpret_cast<const u32x4*>(gsrc + row * FW_N + 8 * cc + 4);
@@ -705,7 +709,7 @@ __global__ __launch_bounds__(FW_THREADS, 1) void first_wgrad_kernel(int64_t kpai
   auto swrite = [&](const St& s, int buf) {
     char* gimg = lds + buf * FW_BUF;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < FW_NG; ++u) {
       const int pr = tid + FW_THREADS * u, row = pr >> 5, cc = pr & 31;
       float v[8];
 #pragma unroll
@@ -738,28 +742,29 @@ __global__ __launch_bounds__(FW_THREADS, 1) void first_wgrad_kernel(int64_t kpai
       }
     }
   };
-  f32x4 acc[4][4];
+  const int fs = wv & 3, cs = wv >> 2;  // the wave's 64-feature slice and 32-column half
+  f32x4 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int q = (lane >> 2) & 3, p = lane & 3, fg = lane >> 4;
   auto mfma_tile = [&](int buf) {
     const char* gk = lds + buf * FW_BUF;
     const char* xk = lds + buf * FW_BUF + 3 * FW_GPS;
-    u32x4 pf[3][4], qf[3][4];
+    u32x4 pf[3][4], qf[3][2];
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int i0 = 64 * wv + 16 * i;
+        const int i0 = 64 * fs + 16 * i;
         pf[pl][i] = tr_frag(gk + pl * FW_GPS + kfrag_off(i0, lane, 0), gk + pl * FW_GPS + kfrag_off(i0, lane, 1));
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        // contraction rows 8 fg + 4 h + q, columns 16 j + 4 p .. + 3
-        const int r0 = 8 * fg + q;
-        qf[pl][j] = tr_frag(xk + pl * FW_XPS + fw_xoff(r0, 16 * j + 4 * p), xk + pl * FW_XPS + fw_xoff(r0 + 4, 16 * j + 4 * p));
+      for (int j = 0; j < 2; ++j) {
+        // contraction rows 8 fg + 4 h + q, columns 16 (2 cs + j) + 4 p .. + 3
+        const int r0 = 8 * fg + q, c0 = 16 * (2 * cs + j) + 4 * p;
+        qf[pl][j] = tr_frag(xk + pl * FW_XPS + fw_xoff(r0, c0), xk + pl * FW_XPS + fw_xoff(r0 + 4, c0));
       }
     }
     constexpr int PP[6] = {2, 0, 1, 1, 0, 0};
@@ -769,7 +774,7 @@ __global__ __launch_bounds__(FW_THREADS, 1) void first_wgrad_kernel(int64_t kpai
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pf[PP[xx]][i]),
                                                               __builtin_bit_cast(bf16x8, qf[QP[xx]][j]), acc[i][j], 0, 0, 0);
   };
@@ -790,16 +795,16 @@ __global__ __launch_bounds__(FW_THREADS, 1) void first_wgrad_kernel(int64_t kpai
     __syncthreads();
     gload(r0);
   }
-  // lane holds D[f = 64 wv + 16 i + 4 fg + r][c = 16 j + fr]; columns past k_in are zero and not stored
+  // lane holds D[f = 64 fs + 16 i + 4 fg + r][c = 16 (2 cs + j) + fr]; columns past k_in are zero and not stored
   const int fr = lane & 15;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int c = 16 * j + fr;
+  for (int j = 0; j < 2; ++j) {
+    const int c = 16 * (2 * cs + j) + fr;
     if (c < k_in) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) partial[((int64_t)b * FW_N + 64 * wv + 16 * i + 4 * fg + r) * k_in + c] = acc[i][j][r];
+        for (int r = 0; r < 4; ++r) partial[((int64_t)b * FW_N + 64 * fs + 16 * i + 4 * fg + r) * k_in + c] = acc[i][j][r];
     }
   }
 }

@@ -104,42 +104,58 @@ struct PartJob {
   const float* src;
   float* dst;
   int64_t parts, part_stride, rows, cols, src_ld, dst_ld;
+  int32_t vec;  // 4: 16-B aligned rows and strides, 4 consecutive columns per lane (float4 loads)
 };
 constexpr int kMaxPartJobs = 16;
 struct PartJobs {
   PartJob j[kMaxPartJobs];
 };
 
-// a block takes 64 consecutive output elements (one per lane); its 4 waves split the parts (wave w: parts
+// a block takes 64 lanes x V consecutive output elements; its 4 waves split the parts (wave w: parts
 // w, w + 4, ...), each lane with 8 independent running sums so that 8 loads are in flight, then the 8 sums,
 // and the 4 waves' sums through LDS, are added in a fixed order (deterministic).  The bias column sums
 // (128-256 parts of 256-512 elements) are then latency-parallel, not one serial chain per column: round 4's
 // one-thread-per-column form of this launch was slower than torch's separate sums.
-__global__ __launch_bounds__(kThreads) void sum_parts_kernel(PartJobs jobs) {
-  __shared__ float red[kThreads / 64][64];
-  const PartJob& J = jobs.j[blockIdx.y];
+template <int V>
+__device__ __forceinline__ void sum_parts_job(const PartJob& J, float (*red)[64 * 4]) {
+  typedef float fv __attribute__((ext_vector_type(V)));
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t len = J.rows * J.cols, e = (int64_t)blockIdx.x * 64 + lane;
-  if ((int64_t)blockIdx.x * 64 >= len) return;  // block-uniform: this job has fewer elements
-  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int64_t len = J.rows * J.cols, e = ((int64_t)blockIdx.x * 64 + lane) * V;
+  fv a[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] = (fv)(0.f);
   if (e < len) {
-    const int64_t r = e / J.cols, c = e - r * J.cols;
+    const int64_t r = e / J.cols, c = e - r * J.cols;  // V | cols: the lane's V columns share one row
     const float* s = J.src + r * J.src_ld + c;
     int64_t q = wv;
     for (; q + 28 < J.parts; q += 32) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) a[u] += s[(q + 4 * u) * J.part_stride];
+      for (int u = 0; u < 8; ++u) a[u] += *reinterpret_cast<const fv*>(s + (q + 4 * u) * J.part_stride);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      if (q + 4 * u < J.parts) a[u] += s[(q + 4 * u) * J.part_stride];
+      if (q + 4 * u < J.parts) a[u] += *reinterpret_cast<const fv*>(s + (q + 4 * u) * J.part_stride);
   }
-  red[wv][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  const fv t = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+#pragma unroll
+  for (int v = 0; v < V; ++v) red[wv][lane * V + v] = t[v];
   __syncthreads();
   if (wv == 0 && e < len) {
     const int64_t r = e / J.cols, c = e - r * J.cols;
-    J.dst[r * J.dst_ld + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    fv o;
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+      o[v] = (red[0][lane * V + v] + red[1][lane * V + v]) + (red[2][lane * V + v] + red[3][lane * V + v]);
+    *reinterpret_cast<fv*>(J.dst + r * J.dst_ld + c) = o;
   }
+}
+
+__global__ __launch_bounds__(kThreads) void sum_parts_kernel(PartJobs jobs) {
+  __shared__ float red[kThreads / 64][64 * 4];
+  const PartJob& J = jobs.j[blockIdx.y];
+  if ((int64_t)blockIdx.x * 64 * J.vec >= J.rows * J.cols) return;  // block-uniform: a shorter job
+  if (J.vec == 4) sum_parts_job<4>(J, red);
+  else sum_parts_job<1>(J, red);
 }
 
 static int blocks_for(int64_t n, int64_t per) {
@@ -194,11 +210,14 @@ int vss_sum_parts(void* stream, int32_t count, const float* const* src, float* c
     if (!src[q] || !dst[q] || parts[q] < 1 || rows[q] < 1 || cols[q] < 1 || src_ld[q] < cols[q] ||
         dst_ld[q] < cols[q] || (parts[q] > 1 && part_stride[q] < rows[q] * src_ld[q] - (src_ld[q] - cols[q])))
       return VSS_E_ARG;
-    jobs.j[q] = vopt::PartJob{src[q], dst[q], parts[q], part_stride[q], rows[q], cols[q], src_ld[q], dst_ld[q]};
-    if (rows[q] * cols[q] > most) most = rows[q] * cols[q];
+    const bool v4 = cols[q] % 4 == 0 && src_ld[q] % 4 == 0 && dst_ld[q] % 4 == 0 && part_stride[q] % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(src[q]) & 15) == 0 && (reinterpret_cast<uintptr_t>(dst[q]) & 15) == 0;
+    jobs.j[q] = vopt::PartJob{src[q], dst[q], parts[q], part_stride[q], rows[q], cols[q], src_ld[q], dst_ld[q], v4 ? 4 : 1};
+    const int64_t nb = (rows[q] * cols[q] + 64 * jobs.j[q].vec - 1) / (64 * jobs.j[q].vec);
+    if (nb > most) most = nb;
   }
-  const int blocks = vopt::blocks_for(most, 64);  // 64 elements per block
-  if (blocks > (1 << 24)) return VSS_E_ARG;
+  const int blocks = (int)most;  // 64 lanes x (1 or 4) elements per block
+  if (most > (1 << 24)) return VSS_E_ARG;
   hipLaunchKernelGGL(vopt::sum_parts_kernel, dim3((unsigned)blocks, (unsigned)count), dim3(vopt::kThreads), 0,
                      (hipStream_t)stream, jobs);
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;

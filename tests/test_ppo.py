@@ -385,16 +385,18 @@ def test_train_is_bit_reproducible_gpu(env_id, tmp_path):
     """The whole loop -- env steps (Philox per field), the rollout policy and its sampling, GAE, the
     captured update minibatches (their replay-12 self-check included), Adam -- run twice with the same
     seed in one process gives the same parameters and the same logged losses, bit for bit: every
-    reduction on the path has a fixed order (no float atomics)."""
-    def run(sub):
+    reduction on the path has a fixed order (no float atomics).  The second run skips the kernel warm-up
+    before the clock (--kernel-warmup false): the warm-up's throwaway loop changes nothing of the run."""
+    def run(sub, warm):
         args = P.parse_args(["--env-id", env_id, "--num-envs", "4095",
                              "--num-steps", "16", "--num-updates", "3", "--seed", "5",
-                             "--save-path", str(tmp_path / sub)])
+                             "--kernel-warmup", str(warm).lower(), "--save-path", str(tmp_path / sub)])
         agent, hist = P.train(args)
+        assert (args.kernel_warmup_s > 0) == warm
         return [p.detach().clone() for p in agent.parameters()], hist
 
-    p1, h1 = run("a")
-    p2, h2 = run("b")
+    p1, h1 = run("a", True)
+    p2, h2 = run("b", False)
     assert all(torch.equal(a, b) for a, b in zip(p1, p2))
     for r1, r2 in zip(h1, h2):
         for k in ("v_loss", "pg_loss", "entropy", "approx_kl"):

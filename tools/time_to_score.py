@@ -58,8 +58,9 @@ def main():
     ap.add_argument("--max-steps", type=float, default=3e8)
     ap.add_argument("--seed", type=int, default=1)
     a = ap.parse_args()
+    # no kernel warm-up: this clock starts before train() and keeps every first use, as in rounds 3-4
     args = P.parse_args(["--env-id", a.env_id, "--num-envs", str(a.num_envs), "--seed", str(a.seed),
-                         "--log", "false"])
+                         "--log", "false", "--kernel-warmup", "false"])
     args.num_updates = int(a.max_steps // args.batch_size)
     cfg = default_cfg(a.eval_fields)
     cfg["env"]["seed"] = 1000 + a.seed

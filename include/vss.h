@@ -326,6 +326,18 @@ int64_t vss_output_backward_chunks(int64_t rows, int32_t k_pad, int32_t n);
 int vss_output_backward(void* stream, int64_t rows, int32_t k_pad, int32_t n, const float* g_out, const float* w_out_t,
                         const float* y, float* grad_in, float* bias_partial, float* wgrad_partial);
 
+/* vss_output_backward_direct: the same pass for the update's minibatch without autograd
+ * (ppo_continuous_action_isaacgym.py direct_minibatch): g_out (rows, k_out) as vss_ppo_loss_direct
+ * writes it and w_out (k_out, n) as nn.Linear holds it -- no padded copies; k_out in {1, 2, 3, 4, 6, 8},
+ * n in {128, 256, 512, 1024}.  bias_partial (chunks, n), wgrad_partial (chunks, k_out, n) with chunks =
+ * vss_output_backward_direct_chunks(rows, k_out, n) <= 256 (-1 for a bad shape), few enough for one
+ * vss_sum_parts launch.  y, grad_in and the partials 16-B aligned; g_out, w_out 4-B aligned.
+ */
+int64_t vss_output_backward_direct_chunks(int64_t rows, int32_t k_out, int32_t n);
+int vss_output_backward_direct(void* stream, int64_t rows, int32_t k_out, int32_t n, const float* g_out,
+                               const float* w_out, const float* y, float* grad_in, float* bias_partial,
+                               float* wgrad_partial);
+
 /* ---------------------------------------------------------------------------------------------
  * The update's hidden-layer GEMMs in fp32 arithmetic on the bf16 matrix cores (csrc/vss_gemm_x6.hip;
  * ppo_continuous_action_isaacgym.py:104-111 under the update's forward ppo…:331 and loss.backward()
@@ -406,6 +418,42 @@ int vss_ppo_loss(void* stream, int64_t rows, int64_t rows_pad, int32_t n_act, co
                  float ent_coef, float vf_coef, int32_t clip_vloss, float* grad_mean, float* grad_value,
                  float* grad_logstd, float* loss_out, float* stats_out, float* partial);
 
+/* vss_ppo_loss_direct: the same loss for the update's minibatch without autograd
+ * (ppo_continuous_action_isaacgym.py direct_minibatch), from what the networks' last launches leave:
+ *   mean_parts (mean_nparts, rows_pad, n_act) + mean_bias (n_act,): the actor's output as the parts of
+ *     vss_linear_tanh_out_bf16x6's out_part (summed in order, then the bias); value_parts
+ *     (value_nparts, rows_pad) + value_bias (1,) the critic's;
+ *   adv (rows,) RAW advantages, normalised in the kernel when adv_part != NULL: adv_part (adv_nparts, 2)
+ *     fp64 (sum, sum of squares) parts over adv_count values (vss_minibatch_gather's, or their all-reduced
+ *     sum), (a - mean) / (std + 1e-8) with mean = s / n, std = sqrt(max((q - n mean^2) / (n - 1), 0)) in
+ *     fp64 (ppo…:325-326, normalize_advantages' data-parallel formula); adv_part NULL: adv as given;
+ *   grad_mean_bias (n_act,), grad_value_bias (1,): the output layers' bias gradients (column sums of
+ *     grad_mean / grad_value, fixed order), written like grad_logstd;
+ * the other arguments as vss_ppo_loss; partial: vss_ppo_loss_direct_scratch_floats(rows_pad, n_act).
+ *
+ * vss_minibatch_gather: one update minibatch's rows (ppo…:310-317) in one launch: for r < rows_pad,
+ *   i = inds[r < mb ? r : (r - mb) % mb] (the padding rows repeat the minibatch), obs[r] = b_obs[i]
+ *   (obs_w floats), act[r] = b_act[i] (act_w floats); for r < mb, logp / adv / ret / val[r] = b_*[i];
+ *   adv_part (vss_minibatch_gather_parts(mb), 2) fp64 (sum, sum of squares) parts of the gathered
+ *   advantages (fixed order).  An index outside [0, batch) gathers NaN.  inds int64 (mb,).
+ * vss_adv_part_sum: out[2] = the nparts parts summed in order (for the data-parallel all-reduce).
+ */
+int64_t vss_ppo_loss_direct_scratch_floats(int64_t rows_pad, int32_t n_act);
+int vss_ppo_loss_direct(void* stream, int64_t rows, int64_t rows_pad, int32_t n_act, const float* mean_parts,
+                        int32_t mean_nparts, const float* mean_bias, const float* value_parts, int32_t value_nparts,
+                        const float* value_bias, const float* logstd, const float* action, const float* logprob_old,
+                        const float* adv, const double* adv_part, int32_t adv_nparts, double adv_count,
+                        const float* returns, const float* values_old, float clip_coef, float clip_lo, float clip_hi,
+                        float ent_coef, float vf_coef, int32_t clip_vloss, float* grad_mean, float* grad_value,
+                        float* grad_logstd, float* grad_mean_bias, float* grad_value_bias, float* loss_out,
+                        float* stats_out, float* partial);
+int64_t vss_minibatch_gather_parts(int64_t mb);
+int vss_minibatch_gather(void* stream, int64_t mb, int64_t rows_pad, int64_t batch, const int64_t* inds, int64_t obs_w,
+                         int64_t act_w, const float* b_obs, const float* b_act, const float* b_logp, const float* b_adv,
+                         const float* b_ret, const float* b_val, float* obs, float* act, float* logp, float* adv,
+                         float* ret, float* val, double* adv_part);
+int vss_adv_part_sum(void* stream, int32_t nparts, const double* part, double* out);
+
 /* ---------------------------------------------------------------------------------------------
  * The update's gradient bookkeeping on flat buffers (csrc/vss_optim.hip; ppo_continuous_action_isaacgym.py
  * FlatParams / FlatGrads / FlatAdam).  Replaces, per minibatch, nn.utils.clip_grad_norm_ (ppo…:353)
@@ -419,7 +467,7 @@ int vss_ppo_loss(void* stream, int64_t rows, int64_t rows_pad, int32_t n_act, co
  *   (>= 1, the count after this step) with torch's fused-Adam arithmetic: m = b1 m + (1 - b1) g,
  *   v = b2 v + (1 - b2) g^2, p -= lr / (1 - b1^step) * m / (sqrt(v) / sqrt(1 - b2^step) + eps).
  *   norm_out (1 float, may be NULL) receives the pre-clip norm.  All buffers n fp32 elements.
- * vss_sum_parts: `count` (1..16) jobs; job q: dst[r * dst_ld + c] = sum over s = 0 .. parts - 1 of
+ * vss_sum_parts: `count` (1..32) jobs; job q: dst[r * dst_ld + c] = sum over s = 0 .. parts - 1 of
  *   src[s * part_stride + r * src_ld + c], r < rows, c < cols, in a fixed order (parts s = w + 4 (u + 8 i)
  *   into running sum (w, u), then those sums in a fixed tree: deterministic).  Host arrays of count
  *   entries; device buffers; src parts must not overlap dst.

@@ -42,27 +42,88 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-template <int NA>
-__global__ __launch_bounds__(kThreads) void loss_rows_kernel(int64_t rows, int64_t rows_pad, const float* __restrict__ mean,
-                                                             const float* __restrict__ logstd, const float* __restrict__ value,
-                                                             const float* __restrict__ action, const float* __restrict__ logp_old,
-                                                             const float* __restrict__ adv, const float* __restrict__ ret,
-                                                             const float* __restrict__ val_old, float clip, float lo, float hi,
-                                                             float vf_coef, int clip_vloss, float inv_n,
-                                                             float* __restrict__ g_mean, float* __restrict__ g_value,
-                                                             float* __restrict__ partial) {
-  constexpr int K = kFixed + NA;
+// the direct form (vss_ppo_loss_direct) reads the networks' outputs as the output layers' epilogue parts
+// and the raw advantages with their normalisation sums, and also sums the output biases' gradients
+struct RowsArgs {
+  int64_t rows, rows_pad;
+  const float* mean;   // (rows_pad, NA); DIRECT: mparts x (rows_pad, NA) epilogue parts of the actor's output
+  const float* value;  // (rows_pad,);    DIRECT: vparts x (rows_pad,) parts of the critic's output
+  int mparts, vparts;
+  const float* b_mean;  // DIRECT: the output layers' biases (NA,) and (1,)
+  const float* b_value;
+  const double* adv_part;  // DIRECT, or NULL: nparts x (sum, sum of squares) of the raw advantages
+  int adv_nparts;
+  double adv_count;
+  const float* logstd;
+  const float* action;
+  const float* logp_old;
+  const float* adv;
+  const float* ret;
+  const float* val_old;
+  float clip, lo, hi, vf_coef;
+  int clip_vloss;
+  float inv_n;
+  float* g_mean;
+  float* g_value;
+  float* partial;
+};
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+// (sum, sum of squares) parts of the advantages -> (mean, std) as fp32, the fp64 formula of
+// normalize_advantages' all-reduced branch (ppo_continuous_action_isaacgym.py): mean = s / n,
+// std = sqrt(max((q - n mean mean) / (n - 1), 0)).  Every block the same fixed order: wave 0's lanes
+// take parts lane, lane + 64, ..., then the wave sum; the result is shared through LDS.
+__device__ __forceinline__ void adv_moments(const double* part, int nparts, double n, float& mean, float& std) {
+  __shared__ float mom[2];
+  if (threadIdx.x < 64) {
+    double s = 0.0, q = 0.0;
+    for (int i = threadIdx.x; i < nparts; i += 64) {
+      s += part[2 * i];
+      q += part[2 * i + 1];
+    }
+    s = wave_sum_f64(s);
+    q = wave_sum_f64(q);
+    if (threadIdx.x == 0) {
+      const double m = s / n;
+      double var = (q - n * m * m) / (n - 1.0);
+      var = var > 0.0 ? var : 0.0;
+      mom[0] = (float)m;
+      mom[1] = (float)sqrt(var);
+    }
+  }
+  __syncthreads();
+  mean = mom[0];
+  std = mom[1];
+}
+
+template <int NA, bool DIRECT>
+__global__ __launch_bounds__(kThreads) void loss_rows_kernel(const RowsArgs p) {
+  // DIRECT also sums the per-row gradients of the actor's means (NA) and of the value (1): the output
+  // layers' bias gradients
+  constexpr int K = kFixed + NA + (DIRECT ? NA + 1 : 0);
   __shared__ float red[kThreads / 64][K];
+  const int64_t rows = p.rows, rows_pad = p.rows_pad;
   // the distribution's per-dimension constants, as torch.distributions.Normal forms them from
   // scale = exp(logstd): var = scale^2, log_scale = log(scale)
-  float var[NA], lsc[NA];
+  float var[NA], lsc[NA], bm[NA];
 #pragma unroll
   for (int a = 0; a < NA; ++a) {
-    const float s = expf(logstd[a]);
+    const float s = expf(p.logstd[a]);
     var[a] = s * s;
     lsc[a] = logf(s);
+    bm[a] = DIRECT ? p.b_mean[a] : 0.f;
   }
+  const float bv = DIRECT ? p.b_value[0] : 0.f;
+  float adv_mean = 0.f, adv_std = 0.f;
+  const bool norm = DIRECT && p.adv_part != nullptr;
+  if (norm) adv_moments(p.adv_part, p.adv_nparts, p.adv_count, adv_mean, adv_std);
   const float log_sqrt_2pi = 0.91893853320467274178f;  // math.log(math.sqrt(2 * math.pi)) as fp32
+  const float inv_n = p.inv_n, clip = p.clip, lo = p.lo, hi = p.hi;
   float acc[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) acc[k] = 0.f;
@@ -70,15 +131,21 @@ __global__ __launch_bounds__(kThreads) void loss_rows_kernel(int64_t rows, int64
   for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < rows_pad; r += stride) {
     if (r >= rows) {  // padding rows: no loss term, no gradient (and no input read)
 #pragma unroll
-      for (int a = 0; a < NA; ++a) g_mean[r * NA + a] = 0.f;
-      g_value[r] = 0.f;
+      for (int a = 0; a < NA; ++a) p.g_mean[r * NA + a] = 0.f;
+      p.g_value[r] = 0.f;
       continue;
     }
     float mu[NA], x[NA];
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-      mu[a] = mean[r * NA + a];
-      x[a] = action[r * NA + a];
+      if constexpr (DIRECT) {  // the output layer's parts, in order, then its bias
+        float m = p.mean[r * NA + a];
+        for (int q = 1; q < p.mparts; ++q) m += p.mean[((int64_t)q * rows_pad + r) * NA + a];
+        mu[a] = m + bm[a];
+      } else {
+        mu[a] = p.mean[r * NA + a];
+      }
+      x[a] = p.action[r * NA + a];
     }
     float nlp = 0.f;
     float dz[NA];
@@ -87,9 +154,10 @@ __global__ __launch_bounds__(kThreads) void loss_rows_kernel(int64_t rows, int64
       dz[a] = x[a] - mu[a];
       nlp += -(dz[a] * dz[a]) / (2.f * var[a]) - lsc[a] - log_sqrt_2pi;
     }
-    const float logratio = nlp - logp_old[r];
+    const float logratio = nlp - p.logp_old[r];
     const float ratio = expf(logratio);
-    const float A = adv[r];
+    float A = p.adv[r];
+    if (norm) A = (A - adv_mean) / (adv_std + 1e-8f);
     acc[2] += -logratio;
     acc[3] += (ratio - 1.f) - logratio;
     acc[4] += fabsf(ratio - 1.f) > clip ? 1.f : 0.f;
@@ -103,13 +171,23 @@ __global__ __launch_bounds__(kThreads) void loss_rows_kernel(int64_t rows, int64
     const float dnlp = dratio * ratio;  // x inv_n for the per-row gradient
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-      g_mean[r * NA + a] = dnlp * inv_n * (dz[a] / var[a]);
+      const float gm = dnlp * inv_n * (dz[a] / var[a]);
+      p.g_mean[r * NA + a] = gm;
       acc[kFixed + a] += dnlp * ((dz[a] * dz[a]) / var[a] - 1.f);
+      if constexpr (DIRECT) acc[kFixed + NA + a] += gm;
     }
-    const float v = value[r], R = ret[r];
+    float v;
+    if constexpr (DIRECT) {
+      v = p.value[r];
+      for (int q = 1; q < p.vparts; ++q) v += p.value[(int64_t)q * rows_pad + r];
+      v += bv;
+    } else {
+      v = p.value[r];
+    }
+    const float R = p.ret[r];
     float dv;
-    if (clip_vloss) {
-      const float vo = val_old[r];
+    if (p.clip_vloss) {
+      const float vo = p.val_old[r];
       const float d = v - vo;
       const float vc = vo + fminf(fmaxf(d, -clip), clip);
       const float eu = v - R, ec = vc - R;
@@ -124,7 +202,9 @@ __global__ __launch_bounds__(kThreads) void loss_rows_kernel(int64_t rows, int64
       acc[1] += e * e;
       dv = e;  // 0.5 x 2 (v - R)
     }
-    g_value[r] = vf_coef * dv * inv_n;
+    const float gv = p.vf_coef * dv * inv_n;
+    p.g_value[r] = gv;
+    if constexpr (DIRECT) acc[kFixed + 2 * NA] += gv;
   }
   // block reduction: wave sums, then the 4 waves' rows in order
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -138,20 +218,21 @@ __global__ __launch_bounds__(kThreads) void loss_rows_kernel(int64_t rows, int64
     float s = red[0][threadIdx.x];
 #pragma unroll
     for (int w = 1; w < kThreads / 64; ++w) s += red[w][threadIdx.x];
-    partial[(int64_t)blockIdx.x * K + threadIdx.x] = s;
+    p.partial[(int64_t)blockIdx.x * K + threadIdx.x] = s;
   }
 }
 
 // one block: the partial rows summed in block order (deterministic), then the losses, the statistics
 // and the log-std gradient.  loss_out[0] = loss; stats_out = [pg_loss, v_loss, entropy_loss,
 // old_approx_kl, approx_kl, clipfrac]
-template <int NA>
+template <int NA, bool DIRECT>
 __global__ __launch_bounds__(kThreads) void loss_finish_kernel(int blocks, const float* __restrict__ logstd,
                                                                float ent_coef, float vf_coef, float n, float inv_n,
                                                                const float* __restrict__ partial,
                                                                float* __restrict__ g_logstd, float* __restrict__ loss_out,
-                                                               float* __restrict__ stats) {
-  constexpr int K = kFixed + NA;
+                                                               float* __restrict__ stats, float* __restrict__ db_mean,
+                                                               float* __restrict__ db_value) {
+  constexpr int K = kFixed + NA + (DIRECT ? NA + 1 : 0);
   __shared__ float tot[K];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // wave wv sums quantities k = wv, wv + 4, ...: lanes stride over the blocks, then a wave sum
@@ -177,6 +258,11 @@ __global__ __launch_bounds__(kThreads) void loss_finish_kernel(int blocks, const
     stats[5] = tot[4] / n;
 #pragma unroll
     for (int a = 0; a < NA; ++a) g_logstd[a] = tot[kFixed + a] * inv_n - ent_coef;
+    if constexpr (DIRECT) {
+#pragma unroll
+      for (int a = 0; a < NA; ++a) db_mean[a] = tot[kFixed + NA + a];
+      db_value[0] = tot[kFixed + 2 * NA];
+    }
   }
 }
 
@@ -185,20 +271,153 @@ static int64_t blocks_for(int64_t rows_pad) {
   return b < 1 ? 1 : (b > kMaxBlocks ? kMaxBlocks : b);
 }
 
-template <int NA>
-static int launch(void* stream, int64_t rows, int64_t rows_pad, const float* mean, const float* logstd,
-                  const float* value, const float* action, const float* logp_old, const float* adv, const float* ret,
-                  const float* val_old, float clip, float lo, float hi, float ent_coef, float vf_coef, int clip_vloss,
-                  float* g_mean, float* g_value, float* g_logstd, float* loss_out, float* stats, float* partial) {
-  const int64_t blocks = blocks_for(rows_pad);
-  const float inv_n = 1.0f / (float)rows;
-  hipLaunchKernelGGL(loss_rows_kernel<NA>, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, rows,
-                     rows_pad, mean, logstd, value, action, logp_old, adv, ret, val_old, clip, lo, hi, vf_coef,
-                     clip_vloss, inv_n, g_mean, g_value, partial);
+template <int NA, bool DIRECT>
+static int launch(void* stream, const RowsArgs& a, float ent_coef, float* g_logstd, float* loss_out, float* stats,
+                  float* db_mean, float* db_value) {
+  const int64_t blocks = blocks_for(a.rows_pad);
+  hipLaunchKernelGGL((loss_rows_kernel<NA, DIRECT>), dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, a);
   if (hipGetLastError() != hipSuccess) return VSS_E_LAUNCH;
-  hipLaunchKernelGGL(loss_finish_kernel<NA>, dim3(1), dim3(kThreads), 0, (hipStream_t)stream, (int)blocks, logstd,
-                     ent_coef, vf_coef, (float)rows, inv_n, partial, g_logstd, loss_out, stats);
+  hipLaunchKernelGGL((loss_finish_kernel<NA, DIRECT>), dim3(1), dim3(kThreads), 0, (hipStream_t)stream, (int)blocks,
+                     a.logstd, ent_coef, a.vf_coef, (float)a.rows, a.inv_n, a.partial, g_logstd, loss_out, stats,
+                     db_mean, db_value);
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+}
+
+template <bool DIRECT>
+static int dispatch(void* stream, int32_t n_act, const RowsArgs& a, float ent_coef, float* g_logstd, float* loss_out,
+                    float* stats, float* db_mean, float* db_value) {
+  switch (n_act) {
+#define VSS_LOSS_CASE(NA) \
+  case NA:                \
+    return launch<NA, DIRECT>(stream, a, ent_coef, g_logstd, loss_out, stats, db_mean, db_value);
+    VSS_LOSS_CASE(1)
+    VSS_LOSS_CASE(2)
+    VSS_LOSS_CASE(3)
+    VSS_LOSS_CASE(4)
+    VSS_LOSS_CASE(6)
+    VSS_LOSS_CASE(8)
+#undef VSS_LOSS_CASE
+    default:
+      return VSS_E_ARG;
+  }
+}
+
+// ---- the minibatch's rows (ppo…:310-317: b_obs[mb_inds], b_actions[mb_inds], b_logprobs[mb_inds],
+// b_advantages[mb_inds], b_returns[mb_inds], b_values[mb_inds]) in ONE launch, with the advantages'
+// (sum, sum of squares) parts for their normalisation (ppo…:325-326), instead of torch's six gathers,
+// a cat and the mean / std chain.  Blocks [0, table_blocks) copy the observation and action rows (rows
+// r >= mb, the update's padding, repeat the minibatch's rows r - mb, r - mb - mb, ...); blocks after them
+// copy the per-row scalars and sum the advantages in fp64, one part per block, in a fixed order.
+constexpr int kGatherTableBlocks = 2048;
+constexpr int kGatherScalarBlocks = 256;
+
+struct GatherArgs {
+  int64_t mb, rows_pad, batch;
+  const int64_t* inds;
+  int64_t obs_w, act_w;  // floats per observation / action row
+  const float* b_obs;
+  const float* b_act;
+  const float* b_logp;
+  const float* b_adv;
+  const float* b_ret;
+  const float* b_val;
+  float* obs;
+  float* act;
+  float* logp;
+  float* adv;
+  float* ret;
+  float* val;
+  double* adv_part;  // (scalar blocks, 2)
+  int table_blocks;
+};
+
+// source row of minibatch row r (the padding rows repeat the minibatch); -1 for an index outside the batch
+__device__ __forceinline__ int64_t src_row(const GatherArgs& g, int64_t r) {
+  const int64_t i = g.inds[r < g.mb ? r : (r - g.mb) % g.mb];
+  return (i >= 0 && i < g.batch) ? i : -1;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kThreads) void gather_kernel(const GatherArgs g) {
+  if ((int)blockIdx.x < g.table_blocks) {
+    const int64_t stride = (int64_t)g.table_blocks * kThreads;
+    const int64_t t0 = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    const float qnan = __builtin_nanf("");
+    if constexpr (VEC) {  // observation rows as 16-B chunks
+      const int64_t cw = g.obs_w / 4;
+      for (int64_t u = t0; u < g.rows_pad * cw; u += stride) {
+        const int64_t r = u / cw, c = u - r * cw;
+        const int64_t i = src_row(g, r);
+        const float4 v = i >= 0 ? reinterpret_cast<const float4*>(g.b_obs + i * g.obs_w)[c]
+                                : make_float4(qnan, qnan, qnan, qnan);
+        reinterpret_cast<float4*>(g.obs + r * g.obs_w)[c] = v;
+      }
+    } else {
+      for (int64_t u = t0; u < g.rows_pad * g.obs_w; u += stride) {
+        const int64_t r = u / g.obs_w, c = u - r * g.obs_w;
+        const int64_t i = src_row(g, r);
+        g.obs[u] = i >= 0 ? g.b_obs[i * g.obs_w + c] : qnan;
+      }
+    }
+    for (int64_t u = t0; u < g.rows_pad * g.act_w; u += stride) {
+      const int64_t r = u / g.act_w, c = u - r * g.act_w;
+      const int64_t i = src_row(g, r);
+      g.act[u] = i >= 0 ? g.b_act[i * g.act_w + c] : qnan;
+    }
+    return;
+  }
+  __shared__ double red[2][kThreads / 64];
+  const int b = (int)blockIdx.x - g.table_blocks, nb = (int)gridDim.x - g.table_blocks;
+  double s = 0.0, q = 0.0;
+  for (int64_t r = (int64_t)b * kThreads + threadIdx.x; r < g.mb; r += (int64_t)nb * kThreads) {
+    const int64_t i = src_row(g, r);
+    if (i < 0) {
+      const float qnan = __builtin_nanf("");
+      g.logp[r] = g.adv[r] = g.ret[r] = g.val[r] = qnan;
+      s += (double)qnan;
+      continue;
+    }
+    const float a = g.b_adv[i];
+    g.logp[r] = g.b_logp[i];
+    g.adv[r] = a;
+    g.ret[r] = g.b_ret[i];
+    g.val[r] = g.b_val[i];
+    s += (double)a;
+    q += (double)a * (double)a;
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  s = wave_sum_f64(s);
+  q = wave_sum_f64(q);
+  if (lane == 0) {
+    red[0][wv] = s;
+    red[1][wv] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double t = red[threadIdx.x][0];
+#pragma unroll
+    for (int w = 1; w < kThreads / 64; ++w) t += red[threadIdx.x][w];
+    g.adv_part[2 * b + threadIdx.x] = t;
+  }
+}
+
+// the parts summed in order into one (sum, sum of squares) pair -- the order adv_moments uses -- for the
+// data-parallel all-reduce of the global statistics
+__global__ void adv_part_sum_kernel(int nparts, const double* __restrict__ part, double* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    double s = 0.0, q = 0.0;
+    for (int i = 0; i < nparts; ++i) {
+      s += part[2 * i];
+      q += part[2 * i + 1];
+    }
+    out[0] = s;
+    out[1] = q;
+  }
+}
+
+static int64_t gather_scalar_blocks(int64_t mb) {
+  int64_t b = (mb + kThreads - 1) / kThreads;
+  return b < 1 ? 1 : (b > kGatherScalarBlocks ? kGatherScalarBlocks : b);
 }
 
 }  // namespace vloss
@@ -218,22 +437,66 @@ int vss_ppo_loss(void* stream, int64_t rows, int64_t rows_pad, int32_t n_act, co
   if (rows <= 0 || rows_pad < rows || !mean || !logstd || !value || !action || !logprob_old || !adv || !returns ||
       !values_old || !grad_mean || !grad_value || !grad_logstd || !loss_out || !stats_out || !partial)
     return VSS_E_ARG;
-  switch (n_act) {
-#define VSS_LOSS_CASE(NA)                                                                                         \
-  case NA:                                                                                                        \
-    return vloss::launch<NA>(stream, rows, rows_pad, mean, logstd, value, action, logprob_old, adv, returns,      \
-                             values_old, clip_coef, clip_lo, clip_hi, ent_coef, vf_coef, clip_vloss, grad_mean,  \
-                             grad_value, grad_logstd, loss_out, stats_out, partial);
-    VSS_LOSS_CASE(1)
-    VSS_LOSS_CASE(2)
-    VSS_LOSS_CASE(3)
-    VSS_LOSS_CASE(4)
-    VSS_LOSS_CASE(6)
-    VSS_LOSS_CASE(8)
-#undef VSS_LOSS_CASE
-    default:
-      return VSS_E_ARG;
-  }
+  const vloss::RowsArgs a{rows, rows_pad, mean, value, 1, 1, nullptr, nullptr, nullptr, 0, 0.0, logstd, action,
+                          logprob_old, adv, returns, values_old, clip_coef, clip_lo, clip_hi, vf_coef, clip_vloss,
+                          1.0f / (float)rows, grad_mean, grad_value, partial};
+  return vloss::dispatch<false>(stream, n_act, a, ent_coef, grad_logstd, loss_out, stats_out, nullptr, nullptr);
+}
+
+int64_t vss_ppo_loss_direct_scratch_floats(int64_t rows_pad, int32_t n_act) {
+  if (rows_pad <= 0 || n_act < 1 || n_act > 8) return -1;
+  return vloss::blocks_for(rows_pad) * (vloss::kFixed + 2 * n_act + 1);
+}
+
+int vss_ppo_loss_direct(void* stream, int64_t rows, int64_t rows_pad, int32_t n_act, const float* mean_parts,
+                        int32_t mean_nparts, const float* mean_bias, const float* value_parts, int32_t value_nparts,
+                        const float* value_bias, const float* logstd, const float* action, const float* logprob_old,
+                        const float* adv, const double* adv_part, int32_t adv_nparts, double adv_count,
+                        const float* returns, const float* values_old, float clip_coef, float clip_lo, float clip_hi,
+                        float ent_coef, float vf_coef, int32_t clip_vloss, float* grad_mean, float* grad_value,
+                        float* grad_logstd, float* grad_mean_bias, float* grad_value_bias, float* loss_out,
+                        float* stats_out, float* partial) {
+  if (rows <= 0 || rows_pad < rows || mean_nparts < 1 || value_nparts < 1 || !mean_parts || !mean_bias ||
+      !value_parts || !value_bias || !logstd || !action || !logprob_old || !adv || !returns || !values_old ||
+      !grad_mean || !grad_value || !grad_logstd || !grad_mean_bias || !grad_value_bias || !loss_out || !stats_out ||
+      !partial || (adv_part && (adv_nparts < 1 || !(adv_count > 1.0))))
+    return VSS_E_ARG;
+  const vloss::RowsArgs a{rows, rows_pad, mean_parts, value_parts, mean_nparts, value_nparts, mean_bias, value_bias,
+                          adv_part, adv_nparts, adv_count, logstd, action, logprob_old, adv, returns, values_old,
+                          clip_coef, clip_lo, clip_hi, vf_coef, clip_vloss, 1.0f / (float)rows, grad_mean, grad_value,
+                          partial};
+  return vloss::dispatch<true>(stream, n_act, a, ent_coef, grad_logstd, loss_out, stats_out, grad_mean_bias,
+                               grad_value_bias);
+}
+
+int64_t vss_minibatch_gather_parts(int64_t mb) { return mb <= 0 ? -1 : vloss::gather_scalar_blocks(mb); }
+
+int vss_minibatch_gather(void* stream, int64_t mb, int64_t rows_pad, int64_t batch, const int64_t* inds, int64_t obs_w,
+                         int64_t act_w, const float* b_obs, const float* b_act, const float* b_logp, const float* b_adv,
+                         const float* b_ret, const float* b_val, float* obs, float* act, float* logp, float* adv,
+                         float* ret, float* val, double* adv_part) {
+  if (mb <= 0 || rows_pad < mb || batch <= 0 || obs_w <= 0 || act_w <= 0 || !inds || !b_obs || !b_act || !b_logp ||
+      !b_adv || !b_ret || !b_val || !obs || !act || !logp || !adv || !ret || !val || !adv_part)
+    return VSS_E_ARG;
+  const int64_t sb = vloss::gather_scalar_blocks(mb);
+  const int64_t units = rows_pad * obs_w;
+  int64_t tb = (units / 4 + vloss::kThreads - 1) / vloss::kThreads;
+  tb = tb < 1 ? 1 : (tb > vloss::kGatherTableBlocks ? vloss::kGatherTableBlocks : tb);
+  const vloss::GatherArgs g{mb, rows_pad, batch, inds, obs_w, act_w, b_obs, b_act, b_logp, b_adv, b_ret, b_val, obs, act,
+                            logp, adv, ret, val, adv_part, (int)tb};
+  const bool vec = obs_w % 4 == 0 && ((reinterpret_cast<uintptr_t>(b_obs) | reinterpret_cast<uintptr_t>(obs)) & 15) == 0;
+  const dim3 grid((unsigned)(tb + sb)), block(vloss::kThreads);
+  if (vec)
+    hipLaunchKernelGGL((vloss::gather_kernel<true>), grid, block, 0, (hipStream_t)stream, g);
+  else
+    hipLaunchKernelGGL((vloss::gather_kernel<false>), grid, block, 0, (hipStream_t)stream, g);
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+}
+
+int vss_adv_part_sum(void* stream, int32_t nparts, const double* part, double* out) {
+  if (nparts < 1 || !part || !out) return VSS_E_ARG;
+  hipLaunchKernelGGL(vloss::adv_part_sum_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (int)nparts, part, out);
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 
 }  // extern "C"

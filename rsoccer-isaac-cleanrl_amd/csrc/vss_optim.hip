@@ -99,16 +99,19 @@ __global__ __launch_bounds__(kThreads) void adam_step_kernel(int64_t n, int32_t 
   }
 }
 
-// one launch for many partial-sum reductions: blockIdx.y = job
+// one launch for many partial-sum reductions: job q owns blocks [first[q], first[q + 1]) of a 1-D grid
+// (no idle blocks for the short jobs)
 struct PartJob {
   const float* src;
   float* dst;
   int64_t parts, part_stride, rows, cols, src_ld, dst_ld;
   int32_t vec;  // 4: 16-B aligned rows and strides, 4 consecutive columns per lane (float4 loads)
 };
-constexpr int kMaxPartJobs = 16;
+constexpr int kMaxPartJobs = 32;
 struct PartJobs {
   PartJob j[kMaxPartJobs];
+  int32_t first[kMaxPartJobs + 1];
+  int32_t count;
 };
 
 // a block takes 64 lanes x V consecutive output elements; its 4 waves split the parts (wave w: parts
@@ -117,10 +120,10 @@ struct PartJobs {
 // (128-256 parts of 256-512 elements) are then latency-parallel, not one serial chain per column: round 4's
 // one-thread-per-column form of this launch was slower than torch's separate sums.
 template <int V>
-__device__ __forceinline__ void sum_parts_job(const PartJob& J, float (*red)[64 * 4]) {
+__device__ __forceinline__ void sum_parts_job(const PartJob& J, int64_t blk, float (*red)[64 * 4]) {
   typedef float fv __attribute__((ext_vector_type(V)));
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t len = J.rows * J.cols, e = ((int64_t)blockIdx.x * 64 + lane) * V;
+  const int64_t len = J.rows * J.cols, e = (blk * 64 + lane) * V;
   fv a[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) a[u] = (fv)(0.f);
@@ -152,10 +155,12 @@ __device__ __forceinline__ void sum_parts_job(const PartJob& J, float (*red)[64 
 
 __global__ __launch_bounds__(kThreads) void sum_parts_kernel(PartJobs jobs) {
   __shared__ float red[kThreads / 64][64 * 4];
-  const PartJob& J = jobs.j[blockIdx.y];
-  if ((int64_t)blockIdx.x * 64 * J.vec >= J.rows * J.cols) return;  // block-uniform: a shorter job
-  if (J.vec == 4) sum_parts_job<4>(J, red);
-  else sum_parts_job<1>(J, red);
+  const int b = (int)blockIdx.x;
+  int q = 0;
+  while (q + 1 < jobs.count && jobs.first[q + 1] <= b) ++q;
+  const PartJob& J = jobs.j[q];
+  if (J.vec == 4) sum_parts_job<4>(J, b - jobs.first[q], red);
+  else sum_parts_job<1>(J, b - jobs.first[q], red);
 }
 
 static int blocks_for(int64_t n, int64_t per) {
@@ -205,7 +210,7 @@ int vss_sum_parts(void* stream, int32_t count, const float* const* src, float* c
       !dst_ld)
     return VSS_E_ARG;
   vopt::PartJobs jobs{};
-  int64_t most = 1;
+  int64_t total = 0;
   for (int q = 0; q < count; ++q) {
     if (!src[q] || !dst[q] || parts[q] < 1 || rows[q] < 1 || cols[q] < 1 || src_ld[q] < cols[q] ||
         dst_ld[q] < cols[q] || (parts[q] > 1 && part_stride[q] < rows[q] * src_ld[q] - (src_ld[q] - cols[q])))
@@ -213,13 +218,14 @@ int vss_sum_parts(void* stream, int32_t count, const float* const* src, float* c
     const bool v4 = cols[q] % 4 == 0 && src_ld[q] % 4 == 0 && dst_ld[q] % 4 == 0 && part_stride[q] % 4 == 0 &&
                     (reinterpret_cast<uintptr_t>(src[q]) & 15) == 0 && (reinterpret_cast<uintptr_t>(dst[q]) & 15) == 0;
     jobs.j[q] = vopt::PartJob{src[q], dst[q], parts[q], part_stride[q], rows[q], cols[q], src_ld[q], dst_ld[q], v4 ? 4 : 1};
-    const int64_t nb = (rows[q] * cols[q] + 64 * jobs.j[q].vec - 1) / (64 * jobs.j[q].vec);
-    if (nb > most) most = nb;
+    const int64_t nb = (rows[q] * cols[q] + 64 * jobs.j[q].vec - 1) / (64 * jobs.j[q].vec);  // 64 lanes x V
+    jobs.first[q] = (int32_t)total;
+    total += nb;
+    if (total > (1 << 24)) return VSS_E_ARG;
   }
-  const int blocks = (int)most;  // 64 lanes x (1 or 4) elements per block
-  if (most > (1 << 24)) return VSS_E_ARG;
-  hipLaunchKernelGGL(vopt::sum_parts_kernel, dim3((unsigned)blocks, (unsigned)count), dim3(vopt::kThreads), 0,
-                     (hipStream_t)stream, jobs);
+  jobs.first[count] = (int32_t)total;
+  jobs.count = count;
+  hipLaunchKernelGGL(vopt::sum_parts_kernel, dim3((unsigned)total), dim3(vopt::kThreads), 0, (hipStream_t)stream, jobs);
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 

@@ -843,6 +843,102 @@ __global__ __launch_bounds__(kSmallThreads) void dtanh_small_k_kernel(int64_t ro
   }
 }
 
+// The direct form (vss_output_backward_direct, the update's minibatch without autograd): g_out read as
+// the loss wrote it (rows, KO), w_out as nn.Linear holds it (KO, n) -- no padded copies -- and blocks of
+// 16 waves, at most kDirMaxBlocks of them, so that the partials (one row of column sums and KO rows of
+// the weight gradient per block) are few enough for the backward's one vss_sum_parts launch.
+constexpr int kDirThreads = 1024;
+constexpr int kDirMaxBlocks = 256;
+
+static SmallPlan direct_plan(int64_t rows, int32_t n) {
+  const int64_t rpp = kDirThreads / (n / 4);
+  int64_t g = (rows + rpp - 1) / rpp;
+  if (g > kDirMaxBlocks) g = kDirMaxBlocks;
+  int64_t per = (rows + g - 1) / g;
+  per = (per + rpp - 1) / rpp * rpp;
+  return SmallPlan{per, (rows + per - 1) / per};
+}
+
+template <int KO>
+__global__ __launch_bounds__(kDirThreads) void output_backward_direct_kernel(int64_t rows, int n,
+                                                                             const float* __restrict__ g,
+                                                                             const float* __restrict__ w,
+                                                                             const float* __restrict__ y,
+                                                                             float* __restrict__ out,
+                                                                             float* __restrict__ partial, int64_t per,
+                                                                             float* __restrict__ wpartial) {
+  __shared__ float4 red[kDirThreads];
+  float4 wacc[KO];
+#pragma unroll
+  for (int a = 0; a < KO; ++a) wacc[a] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int tpr = n >> 2, rpp = kDirThreads / tpr;
+  const int tid = threadIdx.x, c = (tid % tpr) * 4, ro = tid / tpr;
+  float wr[4][KO];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int a = 0; a < KO; ++a) wr[j][a] = w[(int64_t)a * n + c + j];
+  float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int64_t r0 = (int64_t)blockIdx.x * per;
+  const int64_t r1 = r0 + per < rows ? r0 + per : rows;
+  constexpr int U = KO == 1 ? 8 : (KO == 2 ? 6 : (KO <= 4 ? 4 : 2));  // rows in flight per thread (no spill at 1,024 threads)
+  for (int64_t rb = r0 + ro; rb < r1; rb += (int64_t)U * rpp) {
+    float4 yv[U];
+    float gv[U][KO];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = rb + (int64_t)u * rpp;
+      if (row < r1) {
+        yv[u] = *reinterpret_cast<const float4*>(y + row * n + c);
+#pragma unroll
+        for (int a = 0; a < KO; ++a) gv[u][a] = g[row * KO + a];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = rb + (int64_t)u * rpp;
+      if (row < r1) {
+        float acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float t = gv[u][0] * wr[j][0];
+#pragma unroll
+          for (int a = 1; a < KO; ++a) t = fmaf(gv[u][a], wr[j][a], t);
+          acc[j] = t;
+        }
+        const float4 yq = yv[u];
+        const vupd::f32x4 v = {acc[0] * fmaf(-yq.x, yq.x, 1.0f), acc[1] * fmaf(-yq.y, yq.y, 1.0f),
+                               acc[2] * fmaf(-yq.z, yq.z, 1.0f), acc[3] * fmaf(-yq.w, yq.w, 1.0f)};
+        __builtin_nontemporal_store(v, reinterpret_cast<vupd::f32x4*>(out + row * n + c));
+        cs.x += v[0]; cs.y += v[1]; cs.z += v[2]; cs.w += v[3];
+#pragma unroll
+        for (int a = 0; a < KO; ++a) {
+          wacc[a].x = fmaf(gv[u][a], yq.x, wacc[a].x); wacc[a].y = fmaf(gv[u][a], yq.y, wacc[a].y);
+          wacc[a].z = fmaf(gv[u][a], yq.z, wacc[a].z); wacc[a].w = fmaf(gv[u][a], yq.w, wacc[a].w);
+        }
+      }
+    }
+  }
+  red[tid] = cs;
+  __syncthreads();
+  if (tid < tpr) {
+    float4 s4 = red[tid];
+    for (int m = 1; m < rpp; ++m) vupd::add4(s4, red[m * tpr + tid]);
+    *reinterpret_cast<float4*>(partial + (int64_t)blockIdx.x * n + c) = s4;
+  }
+#pragma unroll
+  for (int a = 0; a < KO; ++a) {
+    __syncthreads();
+    red[tid] = wacc[a];
+    __syncthreads();
+    if (tid < tpr) {
+      float4 s4 = red[tid];
+      for (int m = 1; m < rpp; ++m) vupd::add4(s4, red[m * tpr + tid]);
+      *reinterpret_cast<float4*>(wpartial + ((int64_t)blockIdx.x * KO + a) * n + c) = s4;
+    }
+  }
+}
+
 }  // namespace vgemm
 
 extern "C" {
@@ -969,6 +1065,45 @@ int vss_output_backward(void* stream, int64_t rows, int32_t k_pad, int32_t n, co
   else
     hipLaunchKernelGGL((vgemm::dtanh_small_k_kernel<8, true>), grid, block, 0, (hipStream_t)stream, rows, n, g_out,
                        w_out_t, y, grad_in, bias_partial, sp.rows_per_block, wgrad_partial);
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+}
+
+static bool output_direct_ok(int64_t rows, int32_t k_out, int32_t n) {
+  return rows >= 0 && rows <= (int64_t(1) << 40) && (k_out == 1 || k_out == 2 || k_out == 3 || k_out == 4 ||
+                                                      k_out == 6 || k_out == 8) &&
+         n >= 128 && n % 128 == 0 && 1024 % n == 0;
+}
+
+int64_t vss_output_backward_direct_chunks(int64_t rows, int32_t k_out, int32_t n) {
+  if (!output_direct_ok(rows, k_out, n)) return -1;
+  return rows == 0 ? 0 : vgemm::direct_plan(rows, n).blocks;
+}
+
+int vss_output_backward_direct(void* stream, int64_t rows, int32_t k_out, int32_t n, const float* g_out,
+                               const float* w_out, const float* y, float* grad_in, float* bias_partial,
+                               float* wgrad_partial) {
+  if (!output_direct_ok(rows, k_out, n) || !g_out || !w_out || misaligned(y) || misaligned(grad_in) ||
+      misaligned(bias_partial) || misaligned(wgrad_partial))
+    return VSS_E_ARG;
+  if (rows == 0) return VSS_OK;
+  const vgemm::SmallPlan sp = vgemm::direct_plan(rows, n);
+  const dim3 grid((unsigned)sp.blocks), block(vgemm::kDirThreads);
+  switch (k_out) {
+#define VSS_OBD_CASE(KO)                                                                                          \
+  case KO:                                                                                                        \
+    hipLaunchKernelGGL((vgemm::output_backward_direct_kernel<KO>), grid, block, 0, (hipStream_t)stream, rows, n,  \
+                       g_out, w_out, y, grad_in, bias_partial, sp.rows_per_block, wgrad_partial);                 \
+    break;
+    VSS_OBD_CASE(1)
+    VSS_OBD_CASE(2)
+    VSS_OBD_CASE(3)
+    VSS_OBD_CASE(4)
+    VSS_OBD_CASE(6)
+    VSS_OBD_CASE(8)
+#undef VSS_OBD_CASE
+    default:
+      return VSS_E_ARG;
+  }
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 

@@ -55,11 +55,11 @@ from torch.distributions.normal import Normal
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from envs._gym import Box, ObservationWrapper  # noqa: E402
-from vss_amd.loss import ppo_loss  # noqa: E402
+from vss_amd.loss import N_ACT, adv_part_sum, minibatch_gather, minibatch_gather_parts, ppo_loss, ppo_loss_direct  # noqa: E402
 from vss_amd.update import (first_wgrad_ok, gemm_shape_ok, linear_tanh, linear_tanh_backward, linear_tanh_backward_mixed,  # noqa: E402
                             linear_tanh_mixed, linear_tanh_out, linear_tanh_out_mixed, linear_tanh_out_ok,
-                            output_backward, output_backward_ok, sum_parts, weight_grad_mixed, weight_planes,
-                            x6_ok)
+                            linear_tanh_out_x6, output_backward, output_backward_direct, output_backward_direct_ok,
+                            output_backward_ok, sum_parts, weight_grad_mixed, weight_planes, x6_ok)
 
 
 def strtobool(x: str) -> bool:
@@ -245,44 +245,55 @@ class _TanhMLP(torch.autograd.Function):
         defer = [] if gout.is_cuda else None
         gz = gout.contiguous()  # pre-activation gradient of the current layer
         gb = torch.sum(gz, 0, out=dst[2 * n - 1])
-        for layer in reversed(range(n)):
-            if layer == n - 1 and layer > 0 and output_backward_ok(gz.shape[1], hs[layer].shape[1]):
-                # the output layer (1-6 columns): its weight gradient and the backward into the tanh
-                # layer below in one streaming pass over that layer's output (vss_output_backward)
-                grads[2 * layer + 1] = gb
-                gz, gb, grads[2 * layer] = output_backward(gz, ws[layer], hs[layer], out_db=dst[2 * layer - 1],
-                                                           out_dw=dst[2 * layer], defer=defer)
-                continue
-            x6 = gz.is_cuda and UPDATE_GEMM == "x6"
-            if x6 and ((hs[layer].shape[1] % 128 == 0 and gz.shape[1] % 256 == 0) or
-                       (layer == 0 and first_wgrad_ok(256, gz.shape[1], hs[0].shape[1]))):
-                # the hidden layers' and the first layer's weight gradients on the x6 kernels
-                grads[2 * layer] = weight_grad_mixed(gz, hs[layer], out=dst[2 * layer], defer=defer)
-            else:
-                grads[2 * layer] = _split_k_wgrad(gz, hs[layer], out=dst[2 * layer])
-            grads[2 * layer + 1] = gb
-            if layer == 0:
-                break
-            w = ws[layer]
-            if layer == n - 1 and gz.shape[1] % 4:
-                # the output layer's few columns (1, 2 or 6): zero-padded to a multiple of 4, the
-                # GEMM's contraction granule, so this backward is one fused pass as well
-                pad = 4 - gz.shape[1] % 4
-                gz, w = nn.functional.pad(gz, (0, pad)), nn.functional.pad(w, (0, 0, 0, pad))
-            if x6:
-                gz, gb = linear_tanh_backward_mixed(gz, w, hs[layer], out_db=dst[2 * layer - 1],
-                                                    planes=ctx.planes_b.get(layer) if layer < n - 1 else None,
-                                                    defer=defer)
-            else:
-                gz, gb = linear_tanh_backward(gz, w, hs[layer])
-                if dst[2 * layer - 1] is not None:
-                    gb = dst[2 * layer - 1].copy_(gb)
+        top = n - 1
+        if n > 1 and output_backward_ok(gz.shape[1], hs[n - 1].shape[1]):
+            # the output layer (1-6 columns): its weight gradient and the backward into the tanh layer
+            # below in one streaming pass over that layer's output (vss_output_backward)
+            grads[2 * n - 1] = gb
+            gz, gb, grads[2 * n - 2] = output_backward(gz, ws[n - 1], hs[n - 1], out_db=dst[2 * n - 3],
+                                                       out_dw=dst[2 * n - 2], defer=defer)
+            top = n - 2
+        gz = _backward_layers(hs, ws, ctx.planes_b, gz, gb, top, dst, grads, defer)
         if defer:
             sum_parts(defer)
         gx = gz.mm(ws[0]) if ctx.needs_input_grad[0] else None
         # the gradients already written into their parameters' .grad are not handed to autograd
         # (whose AccumulateGrad would add them to themselves)
         return (gx, *[None if d is not None else g for g, d in zip(grads, dst)])
+
+
+def _backward_layers(hs, ws, planes_b, gz, gb, top: int, dst, grads, defer):
+    """Layers top, top - 1, ..., 0 of an MLP backward (_TanhMLP.backward, direct_minibatch): gz = the
+    pre-activation gradient of layer `top`, gb its bias gradient.  Each layer's weight gradient (x6 kernels
+    or the split-K GEMM) into dst / grads, then the backward into the tanh layer below with the tanh
+    derivative and the bias column sums in its epilogue (partial sums queued on `defer` when given).
+    Returns the pre-activation gradient of layer 0."""
+    n = len(ws)
+    for layer in range(top, -1, -1):
+        x6 = gz.is_cuda and UPDATE_GEMM == "x6"
+        if x6 and ((hs[layer].shape[1] % 128 == 0 and gz.shape[1] % 256 == 0) or
+                   (layer == 0 and first_wgrad_ok(256, gz.shape[1], hs[0].shape[1]))):
+            # the hidden layers' and the first layer's weight gradients on the x6 kernels
+            grads[2 * layer] = weight_grad_mixed(gz, hs[layer], out=dst[2 * layer], defer=defer)
+        else:
+            grads[2 * layer] = _split_k_wgrad(gz, hs[layer], out=dst[2 * layer])
+        grads[2 * layer + 1] = gb
+        if layer == 0:
+            break
+        w = ws[layer]
+        if layer == n - 1 and gz.shape[1] % 4:
+            # the output layer's few columns (1, 2 or 6): zero-padded to a multiple of 4, the
+            # GEMM's contraction granule, so this backward is one fused pass as well
+            pad = 4 - gz.shape[1] % 4
+            gz, w = nn.functional.pad(gz, (0, pad)), nn.functional.pad(w, (0, 0, 0, pad))
+        if x6:
+            gz, gb = linear_tanh_backward_mixed(gz, w, hs[layer], out_db=dst[2 * layer - 1],
+                                                planes=planes_b.get(layer) if layer < n - 1 else None, defer=defer)
+        else:
+            gz, gb = linear_tanh_backward(gz, w, hs[layer])
+            if dst[2 * layer - 1] is not None:
+                gb = dst[2 * layer - 1].copy_(gb)
+    return gz
 
 
 def _mlp_planes(ws, rows: int):
@@ -672,6 +683,110 @@ def minibatch_losses(agent, args, obs, actions, logprobs, adv, returns, values):
                     args.ent_coef, args.vf_coef, args.clip_vloss)
 
 
+# ---- the update's minibatch without autograd (round 5) --------------------------------------------------
+# On a ROCm device the minibatch's forward, loss and backward are ONE fixed sequence of this repository's
+# launches (direct_minibatch), not an autograd graph: the output layers' epilogue parts go straight into
+# the loss (vss_ppo_loss_direct: no sum / bias-add launches, the advantage normalisation and the output
+# biases' gradients inside it), the loss's row gradients straight into the output layers' backward
+# (vss_output_backward_direct: no padded copies, no autograd scaling by the loss's incoming gradient of 1),
+# and every gradient is written into its FlatGrads view (no zeroing, no AccumulateGrad); the rows come from
+# one gather launch (vss_minibatch_gather) instead of six gathers, a cat and the mean / std chain.  The
+# kernels are those of the autograd path (_TanhMLP); the results differ from it by summation order only
+# (tests/test_ppo.py::test_direct_minibatch_matches_autograd_path_gpu).
+
+def _mlp_wb(seq: nn.Sequential):
+    lins = list(seq)[0::2]
+    return [m.weight for m in lins], [m.bias for m in lins]
+
+
+def direct_minibatch_ok(agent, args, flat) -> bool:
+    """Whether the update's minibatches run as direct_minibatch: x6 GEMMs, fp32 (no --amp), both MLPs the
+    Agent's (Linear, Tanh) x L + Linear stacks with a 256-wide last hidden layer on the x6 shapes (its
+    output layer's parts feed the loss: 1, 2 or 6 outputs, the actor's n_act in the loss's set, the critic
+    one value), and every parameter's .grad a FlatGrads view on the GPU."""
+    if flat is None or UPDATE_GEMM != "x6" or getattr(args, "amp", "none") != "none":
+        return False
+    for seq, outs in ((agent.actor_mean, N_ACT), (agent.critic, (1,))):
+        if not _fused_mlp_ok(seq):
+            return False
+        ws, _ = _mlp_wb(seq)
+        if len(ws) < 3:
+            return False
+        (n, k), k_out = ws[-2].shape, ws[-1].shape[0]
+        if not (x6_ok(256, k, n) and n == 256 and k_out in (1, 2, 6) and k_out in outs
+                and output_backward_direct_ok(k_out, n)):
+            return False
+    owned = {id(p) for p in flat.params}
+    return all(id(p) in owned and getattr(p, "_vss_flat_grad", False) and p.grad is not None and p.grad.is_cuda
+               and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
+               for p in agent.parameters() if p.requires_grad)
+
+
+def direct_minibatch(agent, args, obs, act, logp, adv, adv_part, adv_count, ret, val):
+    """One update minibatch (ppo…:331-352: the networks, the clipped losses, loss.backward() into the
+    zeroed gradients) as a fixed launch sequence writing every gradient into its FlatGrads view.  obs / act
+    (rows_pad rows, the padding repeating the minibatch), logp / adv / ret / val (rows); adv RAW, normalised
+    inside the loss from adv_part / adv_count (vss_ppo_loss_direct; None: as given).  Returns (loss,
+    (pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac))."""
+    def forward(seq):
+        ws, bs = _mlp_wb(seq)
+        pf, pb = _mlp_planes(ws, obs.shape[0])
+        hs = [obs]
+        for layer in range(len(ws) - 2):
+            hs.append(linear_tanh_mixed(hs[-1], ws[layer], bs[layer], planes=pf.get(layer)))
+        y, parts = linear_tanh_out_x6(hs[-1], ws[-2], bs[-2], ws[-1], bs[-1], planes=pf.get(len(ws) - 2), parts=True)
+        hs.append(y)
+        return hs, ws, bs, parts, pb, [t.grad for w, b in zip(ws, bs) for t in (w, b)]
+
+    def backward(net, g, defer):
+        hs, ws, _, _, pb, d = net
+        n = len(ws)
+        gz, gb, _ = output_backward_direct(g, ws[-1], hs[-1], out_db=d[2 * n - 3], out_dw=d[2 * n - 2], defer=defer)
+        _backward_layers(hs, ws, pb, gz, gb, n - 2, d, [None] * (2 * n), defer)
+
+    # one stream: the critic's launches on a second stream beside the actor's were measured and not kept
+    # (4,095 envs: 0.153 vs 0.154 s per update; 65,536: 2.33 vs 2.30 s -- concurrent GEMMs contend)
+    with torch.no_grad():
+        actor, critic = forward(agent.actor_mean), forward(agent.critic)
+        (_, _, ba, pa, _, da), (_, _, bc, pc, _, dc) = actor, critic
+        g_mean, g_value, loss, stats = ppo_loss_direct(
+            pa, ba[-1], pc, bc[-1], agent.actor_logstd, act, logp, adv, adv_part, adv_count, ret, val, args.clip_coef,
+            args.ent_coef, args.vf_coef, args.clip_vloss, agent.actor_logstd.grad, da[-1], dc[-1])
+        defer = []
+        backward(actor, g_mean, defer)
+        backward(critic, g_value, defer)
+        sum_parts(defer)  # every weight / bias gradient's partial sums, both MLPs, one launch
+    return loss, tuple(stats[i] for i in range(6))
+
+
+class DirectRows:
+    """One minibatch's rows for direct_minibatch: obs / act (rows_pad), logp / adv / ret / val (mb) and the
+    advantages' (sum, sum of squares) parts, filled by gather() (vss_minibatch_gather, one launch)."""
+
+    def __init__(self, mb: int, rows_pad: int, obs_w: int, act_w: int, device):
+        z = lambda *shape, dtype=torch.float32: torch.zeros(shape, device=device, dtype=dtype)  # noqa: E731
+        self.obs, self.act = z(rows_pad, obs_w), z(rows_pad, act_w)
+        self.logp, self.adv, self.ret, self.val = z(mb), z(mb), z(mb), z(mb)
+        self.adv_part = z(minibatch_gather_parts(mb), 2, dtype=torch.float64)
+        self.adv_glob = z(1, 2, dtype=torch.float64)
+
+    def gather(self, inds, b_obs, b_actions, b_logprobs, b_advantages, b_returns, b_values, norm_adv: bool,
+               world: int = 1, global_stats: bool = True):
+        """The rows of inds; returns the (adv_part, adv_count) the loss normalises with: this minibatch's
+        parts, or with several ranks and global_stats their sum all-reduced over the ranks (the union's
+        statistics, as normalize_advantages), or (None, 0) without --norm-adv."""
+        minibatch_gather(inds, b_obs, b_actions, b_logprobs, b_advantages, b_returns, b_values, self.obs, self.act,
+                         self.logp, self.adv, self.ret, self.val, self.adv_part)
+        mb = inds.numel()
+        if not norm_adv:
+            return None, 0.0
+        if world > 1 and global_stats:
+            adv_part_sum(self.adv_part, self.adv_glob)
+            dist.all_reduce(self.adv_glob)
+            return self.adv_glob, float(mb * world)
+        return self.adv_part, float(mb)
+
+
 class MinibatchGraph:
     """One minibatch's forward, losses and backward (into FlatGrads) captured once as a HIP graph and
     replayed for every minibatch: ~300 launches (the MLP GEMMs, the loss and its autograd ops, the
@@ -687,8 +802,15 @@ class MinibatchGraph:
         self.agent, self.flat, self.args = agent, flat, args
         z = lambda *shape: torch.zeros(shape, device=device)  # noqa: E731
         mb_pad = mb + padding_rows(mb, device)
-        self.obs, self.act = z(mb_pad, *obs_dim), z(mb_pad, *act_dim)
-        self.logp, self.adv, self.ret, self.val = z(mb), z(mb), z(mb), z(mb)
+        # direct_minibatch (no autograd) when the networks allow it, with its one-launch gather
+        self.direct = direct_minibatch_ok(agent, args, flat)
+        if self.direct:
+            self.rows = DirectRows(mb, mb_pad, int(np.prod(obs_dim)), int(np.prod(act_dim)), device)
+            self.obs, self.act, self.logp = self.rows.obs, self.rows.act, self.rows.logp
+            self.adv_src = None  # the (adv_part, adv_count) the captured loss reads
+        else:
+            self.obs, self.act = z(mb_pad, *obs_dim), z(mb_pad, *act_dim)
+            self.logp, self.adv, self.ret, self.val = z(mb), z(mb), z(mb), z(mb)
         self.graph = None
         self.warm = False
         self.out = None
@@ -696,6 +818,10 @@ class MinibatchGraph:
         self.failed = False  # a self-check found the replay differing from eager: eager from then on
 
     def _body(self):
+        if self.direct:
+            r = self.rows
+            _, st = direct_minibatch(self.agent, self.args, r.obs, r.act, r.logp, r.adv, *self.adv_src, r.ret, r.val)
+            return st
         loss, st = minibatch_losses(self.agent, self.args, self.obs, self.act, self.logp, self.adv, self.ret,
                                     self.val)
         self.flat.zeroed_backward(loss)
@@ -729,6 +855,23 @@ class MinibatchGraph:
         torch.index_select(b_returns, 0, inds, out=self.ret)
         torch.index_select(b_values, 0, inds, out=self.val)
         self.adv.copy_(mb_adv)
+        return self._step()
+
+    def run_direct(self, inds, b_obs, b_actions, b_logprobs, b_advantages, b_returns, b_values, world: int = 1):
+        """The direct flow: the minibatch's rows gathered into the static buffers in one launch (RAW
+        advantages; the loss normalises them), then the step (replay / eager / capture as run())."""
+        if inds.numel() != self.logp.numel() or b_obs[0].numel() != self.obs.shape[1] or \
+                b_actions[0].numel() != self.act.shape[1]:
+            raise ValueError(f"MinibatchGraph: minibatch {inds.numel()} x {tuple(b_obs.shape[1:])} does not match the "
+                             f"captured {self.logp.numel()} x {self.obs.shape[1]}")
+        src = self.rows.gather(inds, b_obs, b_actions, b_logprobs, b_advantages, b_returns, b_values,
+                               self.args.norm_adv, world, getattr(self.args, "global_adv_norm", True))
+        if self.graph is not None and (src[0] is not self.adv_src[0] or src[1] != self.adv_src[1]):
+            raise ValueError("MinibatchGraph: the advantage normalisation changed after the capture")
+        self.adv_src = src
+        return self._step()
+
+    def _step(self):
         if self.failed:
             return self._body()
         if self.graph is None:
@@ -788,6 +931,47 @@ def make_minibatch_graph(agent, flat, args, batch, obs_dim, act_dim, device):
     return MinibatchGraph(agent, flat, args, mb, obs_dim, act_dim, device)
 
 
+_SIDE_STREAMS = {}
+
+
+class EpochPermutations:
+    """The update's per-epoch minibatch permutations (ppo…:309, torch.randperm(batch) from `gen`, in epoch
+    order).  On a ROCm device with ahead=True (no --target-kl early stop, so every epoch's permutation is
+    drawn), epoch e + 1's is drawn on a side stream while epoch e's minibatches run: torch's randperm is
+    ~25 sort launches (~0.25 ms at 4,095 envs), which then overlap the GEMMs instead of preceding the
+    epoch's first minibatch.  The generator is consumed in the same order: the same permutations."""
+
+    def __init__(self, batch: int, device, gen, epochs: int, ahead: bool = True):
+        self.batch, self.device, self.gen, self.left = batch, torch.device(device), gen, epochs
+        self.side = None
+        if ahead and self.device.type == "cuda":
+            key = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            self.side = _SIDE_STREAMS.setdefault(key, torch.cuda.Stream(device=self.device))
+        self.pending = None
+
+    def _draw(self):
+        self.left -= 1
+        if self.side is None:
+            return torch.randperm(self.batch, device=self.device, generator=self.gen), None
+        main = torch.cuda.current_stream(self.device)
+        self.side.wait_stream(main)  # the generator's state and the allocator: after what main queued so far
+        with torch.cuda.stream(self.side):
+            p = torch.randperm(self.batch, device=self.device, generator=self.gen)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        return p, ev
+
+    def next(self) -> torch.Tensor:
+        p, ev = self.pending if self.pending is not None else self._draw()
+        self.pending = None
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+            p.record_stream(torch.cuda.current_stream(self.device))
+        if self.side is not None and self.left > 0:
+            self.pending = self._draw()  # the next epoch's, overlapping this epoch's minibatches
+        return p
+
+
 def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_advantages, b_returns,
                b_values, world=1, gen=None, graph=None):
     """Clipped PPO over update_epochs x num_minibatches (ppo…:306-365).  Returns last-minibatch
@@ -799,24 +983,41 @@ def ppo_update(agent, optimizer, flat, args, b_obs, b_logprobs, b_actions, b_adv
     pad = padding_rows(mb, device)
     clipfracs = []
     epochs_run = 0
+    # on the GPU with the Agent's networks: direct_minibatch (no autograd), captured or eager alike
+    direct = device.type == "cuda" and MLP_ROW_PAD % 256 == 0 and direct_minibatch_ok(agent, args, flat)
+    rows = {}  # eager direct flow: DirectRows per minibatch size
+    global_stats = getattr(args, "global_adv_norm", True)
+    perms = EpochPermutations(batch, device, gen, args.update_epochs, ahead=args.target_kl is None)
     for epoch in range(args.update_epochs):
         epochs_run += 1
-        b_inds = torch.randperm(batch, device=device, generator=gen)
+        b_inds = perms.next()  # torch.randperm(batch) of ppo…:309, drawn from gen in epoch order
         for start in range(0, batch, mb):
             mb_inds = b_inds[start:start + mb]
-            # the networks' rows: the minibatch, then its first rows again up to the padding
-            inds_pad = mb_inds
-            if pad and mb_inds.numel() == mb:
-                inds_pad = torch.cat([mb_inds, mb_inds.repeat(-(-pad // mb))[:pad]])
-            mb_adv = b_advantages[mb_inds]
-            if args.norm_adv:
-                mb_adv = normalize_advantages(mb_adv, world, getattr(args, "global_adv_norm", True))
-            if graph is not None:
-                st = graph.run(mb_inds, inds_pad, b_obs, b_actions, b_logprobs, mb_adv, b_returns, b_values)
+            if direct and graph is not None and graph.direct and mb_inds.numel() == mb:
+                st = graph.run_direct(mb_inds, b_obs, b_actions, b_logprobs, b_advantages, b_returns, b_values, world)
+            elif direct:
+                m = mb_inds.numel()
+                m_pad = m + padding_rows(m, device)
+                if m not in rows:
+                    rows[m] = DirectRows(m, m_pad, b_obs[0].numel(), b_actions[0].numel(), device)
+                r = rows[m]
+                src = r.gather(mb_inds, b_obs, b_actions, b_logprobs, b_advantages, b_returns, b_values, args.norm_adv,
+                               world, global_stats)
+                _, st = direct_minibatch(agent, args, r.obs, r.act, r.logp, r.adv, *src, r.ret, r.val)
             else:
-                loss, st = minibatch_losses(agent, args, b_obs[inds_pad], b_actions[inds_pad], b_logprobs[mb_inds],
-                                            mb_adv, b_returns[mb_inds], b_values[mb_inds])
-                flat.zeroed_backward(loss)
+                # the networks' rows: the minibatch, then its first rows again up to the padding
+                inds_pad = mb_inds
+                if pad and mb_inds.numel() == mb:
+                    inds_pad = torch.cat([mb_inds, mb_inds.repeat(-(-pad // mb))[:pad]])
+                mb_adv = b_advantages[mb_inds]
+                if args.norm_adv:
+                    mb_adv = normalize_advantages(mb_adv, world, global_stats)
+                if graph is not None:
+                    st = graph.run(mb_inds, inds_pad, b_obs, b_actions, b_logprobs, mb_adv, b_returns, b_values)
+                else:
+                    loss, st = minibatch_losses(agent, args, b_obs[inds_pad], b_actions[inds_pad], b_logprobs[mb_inds],
+                                                mb_adv, b_returns[mb_inds], b_values[mb_inds])
+                    flat.zeroed_backward(loss)
             pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac = st
             clipfracs.append(clipfrac.clone())  # (a graph's outputs are rewritten by the next replay)
             flat.all_reduce_mean(world)  # the data-parallel exchange (RCCL on ROCm)

@@ -40,7 +40,9 @@ EXPORTED = ("vss_abi_version", "vss_source_hash", "vss_error_string", "vss_step"
             "vss_linear_tanh_out_bf16x6", "vss_linear_tanh_backward_chunks_bf16x6", "vss_linear_tanh_backward_bf16x6",
             "vss_weight_grad_chunks_bf16x6", "vss_weight_grad_bf16x6", "vss_first_weight_grad_chunks_bf16x6",
             "vss_first_weight_grad_bf16x6", "vss_weight_planes_bf16x6", "vss_ppo_loss_scratch_floats", "vss_ppo_loss",
-            "vss_grad_sq_partials_count", "vss_grad_sq_partials", "vss_adam_step_clipped", "vss_sum_parts")
+            "vss_grad_sq_partials_count", "vss_grad_sq_partials", "vss_adam_step_clipped", "vss_sum_parts",
+            "vss_output_backward_direct_chunks", "vss_output_backward_direct", "vss_ppo_loss_direct_scratch_floats",
+            "vss_ppo_loss_direct", "vss_minibatch_gather_parts", "vss_minibatch_gather", "vss_adv_part_sum")
 
 
 class VssParams(ctypes.Structure):
@@ -194,6 +196,21 @@ def load() -> ctypes.CDLL:
     L.vss_adam_step_clipped.restype = ctypes.c_int
     L.vss_sum_parts.argtypes = [P, i32] + [P] * 8
     L.vss_sum_parts.restype = ctypes.c_int
+    L.vss_output_backward_direct_chunks.argtypes = [i64, i32, i32]
+    L.vss_output_backward_direct_chunks.restype = i64
+    L.vss_output_backward_direct.argtypes = [P, i64, i32, i32, P, P, P, P, P, P]
+    L.vss_output_backward_direct.restype = ctypes.c_int
+    L.vss_ppo_loss_direct_scratch_floats.argtypes = [i64, i32]
+    L.vss_ppo_loss_direct_scratch_floats.restype = i64
+    L.vss_ppo_loss_direct.argtypes = ([P, i64, i64, i32, P, i32, P, P, i32, P] + [P] * 4 + [P, i32, ctypes.c_double]
+                                      + [P, P] + [f32] * 5 + [i32] + [P] * 8)
+    L.vss_ppo_loss_direct.restype = ctypes.c_int
+    L.vss_minibatch_gather_parts.argtypes = [i64]
+    L.vss_minibatch_gather_parts.restype = i64
+    L.vss_minibatch_gather.argtypes = [P, i64, i64, i64, P, i64, i64] + [P] * 13
+    L.vss_minibatch_gather.restype = ctypes.c_int
+    L.vss_adv_part_sum.argtypes = [P, i32, P, P]
+    L.vss_adv_part_sum.restype = ctypes.c_int
     if L.vss_abi_version() != ABI_VERSION:
         raise NativeError(f"libvss_amd ABI {L.vss_abi_version()} != expected {ABI_VERSION}")
     _lib = L

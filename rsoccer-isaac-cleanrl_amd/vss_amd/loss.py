@@ -112,3 +112,85 @@ def ppo_loss(mean, logstd, value, action, logprob_old, adv, returns, values_old,
     loss, stats = _PPOLoss.apply(mean, logstd, value.reshape(-1, 1), action[:mean.shape[0]], logprob_old, adv, returns,
                                  values_old, clip_coef, ent_coef, vf_coef, clip_vloss)
     return loss, tuple(stats[i] for i in range(6))
+
+
+# ---- the update's minibatch without autograd (ppo_continuous_action_isaacgym.py direct_minibatch) -------
+
+def ppo_loss_direct(mean_parts, mean_bias, value_parts, value_bias, logstd, action, logprob_old, adv, adv_part,
+                    adv_count, returns, values_old, clip_coef, ent_coef, vf_coef, clip_vloss, grad_logstd,
+                    grad_mean_bias, grad_value_bias):
+    """vss_ppo_loss_direct: the loss from the output layers' epilogue parts -- mean_parts (P, rows_pad,
+    n_act) + mean_bias, value_parts (Q, rows_pad, 1) + value_bias -- and the RAW advantages, normalised in
+    the kernel from adv_part ((parts, 2) fp64 (sum, sum of squares) over adv_count values; None: adv is
+    used as given).  Writes d loss / d logstd and the output layers' bias gradients into grad_logstd,
+    grad_mean_bias, grad_value_bias (the FlatGrads views); returns (grad_mean (rows_pad, n_act),
+    grad_value (rows_pad, 1), loss, stats (6,))."""
+    rows = logprob_old.shape[0]
+    nm, rows_pad, n_act = mean_parts.shape
+    nv = value_parts.shape[0]
+    if n_act not in N_ACT or value_parts.shape[1] != rows_pad or value_parts.numel() != nv * rows_pad \
+            or action.shape[0] < rows_pad or action.shape[1] != n_act or not 0 < rows <= rows_pad \
+            or mean_bias.numel() != n_act or value_bias.numel() != 1 or logstd.numel() != n_act \
+            or grad_logstd.numel() != n_act or grad_mean_bias.numel() != n_act or grad_value_bias.numel() != 1 \
+            or not (adv.shape == returns.shape == values_old.shape == logprob_old.shape):
+        raise ValueError(f"ppo_loss_direct: mean parts {tuple(mean_parts.shape)}, value parts {tuple(value_parts.shape)}, "
+                         f"action {tuple(action.shape)}, rows {rows}")
+    ts = (mean_parts, mean_bias, value_parts, value_bias, logstd, action, logprob_old, adv, returns, values_old,
+          grad_logstd, grad_mean_bias, grad_value_bias)
+    for t in ts:
+        if t.dtype != torch.float32 or t.device != mean_parts.device or not t.is_contiguous():
+            raise ValueError(f"ppo_loss_direct: contiguous fp32 tensors on {mean_parts.device}, got {t.dtype} on {t.device}")
+    if adv_part is not None and (adv_part.dtype != torch.float64 or adv_part.device != mean_parts.device
+                                 or adv_part.dim() != 2 or adv_part.shape[1] != 2 or not adv_part.is_contiguous()):
+        raise ValueError("ppo_loss_direct: adv_part must be a contiguous (parts, 2) fp64 tensor on the same device")
+    lib = N.load()
+    dev = mean_parts.device
+    f32 = dict(device=dev, dtype=torch.float32)
+    g_mean = torch.empty((rows_pad, n_act), **f32)
+    g_value = torch.empty((rows_pad, 1), **f32)
+    loss = torch.empty((), **f32)
+    stats = torch.empty(6, **f32)
+    part = torch.empty(lib.vss_ppo_loss_direct_scratch_floats(rows_pad, n_act), **f32)
+    c = float(clip_coef)
+    N.check(lib.vss_ppo_loss_direct(
+        N.stream_of(dev), rows, rows_pad, n_act, mean_parts.data_ptr(), nm, mean_bias.data_ptr(), value_parts.data_ptr(),
+        nv, value_bias.data_ptr(), logstd.data_ptr(), action.data_ptr(), logprob_old.data_ptr(), adv.data_ptr(),
+        adv_part.data_ptr() if adv_part is not None else None, adv_part.shape[0] if adv_part is not None else 0,
+        float(adv_count), returns.data_ptr(), values_old.data_ptr(), c, 1 - c, 1 + c, float(ent_coef), float(vf_coef),
+        int(bool(clip_vloss)), g_mean.data_ptr(), g_value.data_ptr(), grad_logstd.data_ptr(), grad_mean_bias.data_ptr(),
+        grad_value_bias.data_ptr(), loss.data_ptr(), stats.data_ptr(), part.data_ptr()), "vss_ppo_loss_direct")
+    return g_mean, g_value, loss, stats
+
+
+def minibatch_gather_parts(mb: int) -> int:
+    """Rows of the (sum, sum of squares) parts minibatch_gather writes for mb minibatch rows."""
+    return int(N.load().vss_minibatch_gather_parts(mb))
+
+
+def minibatch_gather(inds, b_obs, b_act, b_logp, b_adv, b_ret, b_val, obs, act, logp, adv, ret, val, adv_part):
+    """vss_minibatch_gather: the minibatch rows inds (int64, mb) of the batch tensors into obs / act
+    (rows_pad >= mb rows: the padding rows repeat the minibatch's) and logp / adv / ret / val (mb), with
+    the advantages' fp64 (sum, sum of squares) parts in adv_part ((minibatch_gather_parts(mb), 2)), in one
+    launch (ppo…:310-317 b_obs[mb_inds] ... and the sums of ppo…:325-326's normalisation)."""
+    mb, rows_pad, batch = inds.numel(), obs.shape[0], b_obs.shape[0]
+    bo, ba = b_obs.reshape(batch, -1), b_act.reshape(batch, -1)
+    ow, aw = bo.shape[1], ba.shape[1]
+    f32 = (b_obs, b_act, b_logp, b_adv, b_ret, b_val, obs, act, logp, adv, ret, val)
+    if inds.dtype != torch.int64 or not inds.is_contiguous() or not inds.is_cuda or rows_pad < mb or mb == 0 \
+            or obs.reshape(rows_pad, -1).shape[1] != ow or act.shape[0] != rows_pad or act.reshape(rows_pad, -1).shape[1] != aw \
+            or any(t.numel() != mb for t in (logp, adv, ret, val)) or any(t.shape[0] != batch for t in f32[:6]) \
+            or adv_part.dtype != torch.float64 or adv_part.numel() != 2 * minibatch_gather_parts(mb) \
+            or any(t.dtype != torch.float32 or not t.is_contiguous() or t.device != inds.device for t in f32):
+        raise ValueError(f"minibatch_gather: {mb} indices into a batch of {batch} x {ow} / {aw}, outputs of "
+                         f"{rows_pad} rows")
+    N.check(N.load().vss_minibatch_gather(N.stream_of(inds.device), mb, rows_pad, batch, inds.data_ptr(), ow, aw,
+                                          *[t.data_ptr() for t in f32], adv_part.data_ptr()), "vss_minibatch_gather")
+
+
+def adv_part_sum(adv_part: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out (1, 2) fp64 = adv_part's rows summed in order (the data-parallel all-reduce's operand)."""
+    if adv_part.dtype != torch.float64 or out.dtype != torch.float64 or out.numel() != 2 or adv_part.dim() != 2:
+        raise ValueError("adv_part_sum: fp64 (parts, 2) -> (1, 2)")
+    N.check(N.load().vss_adv_part_sum(N.stream_of(out.device), adv_part.shape[0], adv_part.data_ptr(), out.data_ptr()),
+            "vss_adv_part_sum")
+    return out

@@ -88,11 +88,12 @@ def _reduce_parts(parts: torch.Tensor, out: torch.Tensor | None, defer: list | N
 
 def sum_parts(jobs) -> None:
     """jobs = [(parts (S, ...) fp32, out (...) fp32)]: out = parts.sum(0) for all of them in one launch
-    per 16 jobs (vss_sum_parts; parts summed in order s = 0 .. S-1, deterministic).  `out` may be a
+    per 32 jobs (vss_sum_parts; parts summed in order s = 0 .. S-1, deterministic).  `out` may be a
     row-strided 2-D view; the last dim of both must be contiguous."""
-    jobs = list(jobs)
-    for q0 in range(0, len(jobs), 16):
-        chunk = jobs[q0:q0 + 16]
+    # the longest part lists first: their blocks (the longest serial chains) start first
+    jobs = sorted(jobs, key=lambda j: -j[0].shape[0])
+    for q0 in range(0, len(jobs), 32):
+        chunk = jobs[q0:q0 + 32]
         cols = {k: [] for k in ("src", "dst", "parts", "pstride", "rows", "cols", "sld", "dld")}
         for parts, out in chunk:
             p3 = parts.reshape(parts.shape[0], -1, parts.shape[-1]) if parts.dim() >= 2 else None
@@ -233,6 +234,36 @@ def output_backward(g_out: torch.Tensor, w_out: torch.Tensor, y: torch.Tensor, o
     return gz, _reduce_parts(bpart, out_db, defer), _reduce_parts(wpart[:, :k_out], out_dw, defer)
 
 
+def output_backward_direct_ok(k_out: int, n: int) -> bool:
+    """Shapes vss_output_backward_direct takes: k_out in {1, 2, 3, 4, 6, 8}, n in {128, 256, 512, 1024}."""
+    return k_out in (1, 2, 3, 4, 6, 8) and n >= 128 and n % 128 == 0 and 1024 % n == 0
+
+
+def output_backward_direct(g_out: torch.Tensor, w_out: torch.Tensor, y: torch.Tensor, out_db: torch.Tensor | None = None,
+                           out_dw: torch.Tensor | None = None, defer: list | None = None):
+    """output_backward for the update's minibatch without autograd (vss_output_backward_direct): g_out
+    (rows, k_out) and w_out (k_out, n) as they are (no padded copies), at most 256 partial rows, so the
+    bias and weight gradients join the backward's sum_parts launch (defer).  Returns (gz, db, dw)."""
+    rows, k_out = g_out.shape
+    n = y.shape[1]
+    if w_out.shape != (k_out, n) or y.shape[0] != rows or not output_backward_direct_ok(k_out, n):
+        raise ValueError(f"output_backward_direct: g_out {tuple(g_out.shape)}, w_out {tuple(w_out.shape)}, y {tuple(y.shape)}")
+    _x6_check("vss_output_backward_direct", True, g_out, w_out, y)
+    lib = N.load()
+    g_out, w_out, y = g_out.contiguous(), w_out.contiguous(), y.contiguous()
+    gz = torch.empty((rows, n), device=y.device, dtype=torch.float32)
+    chunks = lib.vss_output_backward_direct_chunks(rows, k_out, n)
+    bpart = torch.empty((max(chunks, 1), n), device=y.device, dtype=torch.float32)
+    wpart = torch.empty((max(chunks, 1), k_out, n), device=y.device, dtype=torch.float32)
+    if rows == 0:
+        bpart.zero_()
+        wpart.zero_()
+    N.check(lib.vss_output_backward_direct(N.stream_of(y.device), rows, k_out, n, g_out.data_ptr(), w_out.data_ptr(),
+                                           y.data_ptr(), gz.data_ptr(), bpart.data_ptr(), wpart.data_ptr()),
+            "vss_output_backward_direct")
+    return gz, _reduce_parts(bpart, out_db, defer), _reduce_parts(wpart, out_dw, defer)
+
+
 # ---- the same GEMMs in fp32 arithmetic on the bf16 matrix cores (csrc/vss_gemm_x6.hip) ----------------
 # Every operand is split exactly into three bf16 parts and each product is summed from the six partial
 # products above 2^-23 |a||b| in fp32 (tests/test_gemm_x6.py: the error is that of an fp32 GEMM).
@@ -319,8 +350,10 @@ def linear_tanh_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch
 
 
 def linear_tanh_out_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out: torch.Tensor, b_out: torch.Tensor,
-                       out: torch.Tensor | None = None, planes: torch.Tensor | None = None):
-    """linear_tanh_out on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_out_bf16x6)."""
+                       out: torch.Tensor | None = None, planes: torch.Tensor | None = None, parts: bool = False):
+    """linear_tanh_out on the bf16 matrix cores with fp32 arithmetic (vss_linear_tanh_out_bf16x6).
+    parts: return (y, the output layer's epilogue parts (n // 64, rows, k_out)) without summing them or
+    adding b_out -- vss_ppo_loss_direct reads them as they are."""
     rows, k = x.shape
     n, k_out = w.shape[0], w_out.shape[0]
     _x6_check("vss_linear_tanh_out_bf16x6", w.shape == (n, k) and b.shape == (n,) and w_out.shape == (k_out, n)
@@ -333,6 +366,8 @@ def linear_tanh_out_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out:
                                                 b.data_ptr(), y.data_ptr(), k_out, w_out.data_ptr(), part.data_ptr(),
                                                 pp), "vss_linear_tanh_out_bf16x6")
     del keep  # the split and the GEMM are queued: the scratch may be reused from here on
+    if parts:
+        return y, part
     return y, part.sum(0).add_(b_out)
 
 

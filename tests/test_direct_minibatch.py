@@ -1,0 +1,170 @@
+"""The update's minibatch without autograd (ppo_continuous_action_isaacgym.py direct_minibatch, round 5):
+its three new launches -- the one-launch row gather with the advantages' fp64 sums
+(vss_minibatch_gather), the loss from the output layers' epilogue parts with the advantage normalisation
+and the output biases' gradients inside (vss_ppo_loss_direct), the output layer's backward without padded
+copies (vss_output_backward_direct) -- each against its torch / autograd-path counterpart, and the whole
+direct minibatch against the autograd path (minibatch_losses + FlatGrads.zeroed_backward, which the
+CPU suite and the other shapes keep)."""
+import numpy as np
+import pytest
+import torch
+
+import ppo_continuous_action_isaacgym as P
+from test_ppo import _args, _synthetic_batch, make_agent
+from vss_amd.loss import N_ACT, adv_part_sum, minibatch_gather, minibatch_gather_parts, ppo_loss, ppo_loss_direct
+from vss_amd.update import output_backward, output_backward_direct, output_backward_direct_ok
+
+
+def test_direct_shapes_cpu():
+    """The shapes the direct launches take, and the gather's part count (host-side, no GPU)."""
+    assert all(output_backward_direct_ok(k, 256) for k in (1, 2, 3, 4, 6, 8))
+    assert not output_backward_direct_ok(5, 256) and not output_backward_direct_ok(2, 384)
+    assert minibatch_gather_parts(1) == 1 and minibatch_gather_parts(131040) == 256
+    assert N_ACT == (1, 2, 3, 4, 6, 8)
+
+
+def test_direct_minibatch_not_for_cpu_or_amp():
+    """direct_minibatch_ok: FlatGrads-owned GPU gradients, fp32 networks -- CPU agents and --amp keep the
+    autograd path."""
+    agent = make_agent(2)
+    flat = P.FlatGrads(agent)
+    assert not P.direct_minibatch_ok(agent, _args(), flat)  # CPU gradients
+    assert not P.direct_minibatch_ok(agent, _args(), None)
+    assert not P.direct_minibatch_ok(agent, _args(amp="bf16"), flat)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mb,rows_pad,obs_w", [(1000, 1024, 52), (131040, 131072, 52), (300, 512, 7)])
+def test_minibatch_gather_matches_index_select_gpu(mb, rows_pad, obs_w):
+    """vss_minibatch_gather = index_select of every batch tensor (the padding rows repeating the
+    minibatch's rows), bit for bit; the advantages' parts sum to their fp64 sum and sum of squares; an
+    index outside the batch gathers NaN (no out-of-bounds read)."""
+    batch = 3 * mb + 17
+    g = torch.Generator(device="cuda").manual_seed(1)
+    b_obs = torch.randn(batch, obs_w, device="cuda", generator=g)
+    b_act = torch.randn(batch, 2, device="cuda", generator=g)
+    b_s = [torch.randn(batch, device="cuda", generator=g) for _ in range(4)]
+    inds = torch.randperm(batch, device="cuda", generator=g)[:mb].contiguous()
+    z = lambda *s, dt=torch.float32: torch.full(s, 5.0, device="cuda", dtype=dt)  # noqa: E731
+    obs, act, outs = z(rows_pad, obs_w), z(rows_pad, 2), [z(mb) for _ in range(4)]
+    part = z(minibatch_gather_parts(mb), 2, dt=torch.float64)
+    minibatch_gather(inds, b_obs, b_act, *b_s, obs, act, *outs, part)
+    pad_inds = torch.cat([inds, inds.repeat(rows_pad // mb + 1)[:rows_pad - mb]])
+    assert torch.equal(obs, b_obs[pad_inds]) and torch.equal(act, b_act[pad_inds])
+    for o, b in zip(outs, b_s):
+        assert torch.equal(o, b[inds])
+    a = b_s[1][inds].double()  # the advantages (logp, adv, ret, val order)
+    tot = adv_part_sum(part, torch.empty(1, 2, device="cuda", dtype=torch.float64))
+    np.testing.assert_allclose(tot.cpu().numpy()[0], [float(a.sum()), float((a * a).sum())], rtol=1e-12, atol=1e-9)
+    bad = inds.clone()
+    bad[3] = batch + 5
+    minibatch_gather(bad, b_obs, b_act, *b_s, obs, act, *outs, part)
+    assert torch.isnan(obs[3]).all() and torch.isnan(outs[0][3]) and not torch.isnan(obs[4]).any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k_out", [1, 2, 6])
+def test_output_backward_direct_matches_padded_pass_gpu(k_out):
+    """vss_output_backward_direct (g_out and w_out as they are, <= 256 parts) = vss_output_backward on the
+    zero-padded copies: the same gradient bits (the padding adds exact zeros), the bias and weight
+    gradients within fp32 summation-order rounding."""
+    rows, n = 131072, 256
+    g = torch.Generator(device="cuda").manual_seed(2)
+    go = torch.randn(rows, k_out, device="cuda", generator=g) * 1e-3
+    w = torch.randn(k_out, n, device="cuda", generator=g) / 16
+    y = torch.tanh(torch.randn(rows, n, device="cuda", generator=g))
+    gz0, db0, dw0 = output_backward(go, w, y)
+    defer = []
+    gz1, db1, dw1 = output_backward_direct(go, w, y, defer=defer)
+    assert len(defer) == 2 and all(p.shape[0] <= 256 for p, _ in defer)
+    P.sum_parts(defer)
+    assert torch.equal(gz0, gz1)
+    ref_db, ref_dw = (go.double() @ w.double() * (1 - y.double() ** 2)).sum(0), go.double().t() @ y.double()
+    for got, want in ((db0, ref_db), (db1, ref_db), (dw0, ref_dw), (dw1, ref_dw)):
+        assert float((got.double() - want).abs().max()) <= 1e-5 * float(want.abs().max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("norm,clip_vloss", [(True, False), (True, True), (False, True)])
+def test_ppo_loss_direct_matches_loss_on_summed_outputs_gpu(norm, clip_vloss):
+    """vss_ppo_loss_direct on the epilogue parts + biases and the RAW advantages = vss_ppo_loss on the
+    summed outputs and the advantages normalised with the same fp64 statistics: the same losses, row
+    gradients and log-std gradient; the output biases' gradients = the row gradients' column sums."""
+    rows, rows_pad, n_act = 131040, 131072, 2
+    g = torch.Generator(device="cuda").manual_seed(3)
+    mp = torch.randn(4, rows_pad, n_act, device="cuda", generator=g) * 0.1
+    vp = torch.randn(4, rows_pad, 1, device="cuda", generator=g)
+    bm, bv = torch.randn(n_act, device="cuda", generator=g) * 0.1, torch.randn(1, device="cuda", generator=g)
+    logstd = torch.randn(1, n_act, device="cuda", generator=g) * 0.1
+    act = torch.randn(rows_pad, n_act, device="cuda", generator=g) * 0.3
+    logp, adv, ret, val = [torch.randn(rows, device="cuda", generator=g) for _ in range(4)]
+    logp = logp - 1.0
+    part = None
+    if norm:
+        a = adv.double()
+        part = torch.stack([a.sum(), (a * a).sum()]).view(1, 2).contiguous()
+        m = part[0, 0] / rows
+        sd = ((part[0, 1] - rows * m * m) / (rows - 1)).clamp(min=0).sqrt()
+        adv_n = (adv - m.float()) / (sd.float() + 1e-8)
+    else:
+        adv_n = adv
+    mean = mp.sum(0) + bm
+    value = vp.sum(0) + bv
+    loss0, st0 = ppo_loss(mean.requires_grad_(), logstd.requires_grad_(), value.requires_grad_(), act, logp, adv_n,
+                          ret, val, 0.2, 0.01, 0.5, clip_vloss)
+    loss0.backward()
+    gl, dbm, dbv = torch.empty_like(logstd), torch.empty(n_act, device="cuda"), torch.empty(1, device="cuda")
+    gm, gv, loss1, st1 = ppo_loss_direct(mp, bm, vp, bv, logstd.detach(), act, logp, adv, part, rows, ret, val,
+                                         0.2, 0.01, 0.5, clip_vloss, gl, dbm, dbv)
+    torch.testing.assert_close(loss1, loss0.detach(), rtol=2e-6, atol=1e-7)
+    torch.testing.assert_close(st1, torch.stack([t.detach() for t in st0]), rtol=2e-6, atol=1e-7)
+    scale_m, scale_v = float(mean.grad.abs().max()), float(value.grad.abs().max())
+    assert float((gm - mean.grad).abs().max()) <= 1e-5 * scale_m
+    assert float((gv - value.grad).abs().max()) <= 1e-5 * scale_v
+    torch.testing.assert_close(gl, logstd.grad, rtol=1e-5, atol=1e-7)
+    assert float((dbm.double() - gm.double().sum(0)).abs().max()) <= 1e-6 * float(gm.double().abs().sum())
+    assert float((dbv.double() - gv.double().sum()).abs().max()) <= 1e-6 * float(gv.double().abs().sum())
+
+
+def _grads(agent):
+    return [p.grad.detach().clone() for p in agent.parameters()]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,nmb,act_dim,norm_adv,clip_vloss", [
+    (262080, 2, 2, True, False),   # 131,040-row minibatches (4,095 envs): 32 padding rows
+    (32768, 2, 2, True, True), (32768, 4, 6, False, True), (4096, 2, 2, True, False)])
+def test_direct_minibatch_matches_autograd_path_gpu(n, nmb, act_dim, norm_adv, clip_vloss):
+    """One minibatch through direct_minibatch (gather, forward, loss, backward into the FlatGrads views)
+    against the autograd path on the same rows (index_select + normalize_advantages + minibatch_losses +
+    zeroed_backward): every parameter's gradient within 2e-5 of its largest entry, the statistics within
+    fp32 rounding; every gradient view written (the flat buffer starts as NaN)."""
+    args = _args(norm_adv=norm_adv, clip_vloss=clip_vloss, num_minibatches=nmb)
+    g = torch.Generator().manual_seed(11)
+    obs, _, logp, adv, ret, val = [t.cuda() for t in _synthetic_batch(5, n)]
+    act = (torch.randn(n, act_dim, generator=g) * 0.5).cuda()
+    agent = make_agent(act_dim).cuda()
+    flat = P.FlatGrads(agent)
+    assert P.direct_minibatch_ok(agent, args, flat)
+    mb = n // nmb
+    inds = torch.randperm(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(4))[:mb]
+    pad = P.padding_rows(mb, "cuda")
+    inds_pad = torch.cat([inds, inds.repeat(-(-pad // mb))[:pad]]) if pad else inds
+    mb_adv = P.normalize_advantages(adv[inds]) if norm_adv else adv[inds]
+    loss, st0 = P.minibatch_losses(agent, args, obs[inds_pad], act[inds_pad], logp[inds], mb_adv, ret[inds], val[inds])
+    flat.zeroed_backward(loss)
+    want = _grads(agent)
+    flat.flat.fill_(float("nan"))
+    rows = P.DirectRows(mb, mb + pad, 52, act_dim, "cuda")
+    src = rows.gather(inds, obs, act, logp, adv, ret, val, norm_adv)
+    _, st1 = P.direct_minibatch(agent, args, rows.obs, rows.act, rows.logp, rows.adv, *src, rows.ret, rows.val)
+    got = _grads(agent)
+    for (name, _), a, b in zip(agent.named_parameters(), want, got):
+        assert not torch.isnan(b).any(), name
+        assert float((a - b).abs().max()) <= 2e-5 * float(a.abs().max()) + 1e-12, name
+    for a, b in zip(st0, st1):
+        assert abs(float(a) - float(b)) <= 2e-5 * max(abs(float(a)), 1e-3)
+    # the same minibatch again: the same bits (no atomics, fixed orders)
+    _, st2 = P.direct_minibatch(agent, args, rows.obs, rows.act, rows.logp, rows.adv, *src, rows.ret, rows.val)
+    assert all(torch.equal(a, b) for a, b in zip(got, _grads(agent)))
+    assert all(float(a) == float(b) for a, b in zip(st1, st2))

@@ -293,7 +293,9 @@ def test_minibatch_graph_self_check_gpu(corrupt):
                 def replay(self):
                     self.g.replay()
                     if graph.replays + 1 >= bad_replay:
-                        flat.flat[7] += 1.0
+                        # a gradient element (flat[7] itself is alignment padding after actor_logstd's
+                        # 2 floats: the direct minibatch writes every gradient but never the padding)
+                        agent.critic[0].weight.grad.view(-1)[7] += 1.0
 
             def capture_and_corrupt():
                 capture()
@@ -668,8 +670,9 @@ def test_flat_adam_zero_grad_keeps_the_flat_views_gpu():
 @pytest.mark.gpu
 def test_sum_parts_matches_torch_sum_gpu():
     """vss_sum_parts (one launch for many part reductions): 3-D parts into a contiguous and a row-strided
-    out, 2-D parts into a 1-D out (also 256 parts of 512 columns: the bias column sums' shape); equal to the
-    parts summed one after another within fp32 summation-order rounding, and the same bits on a repeat."""
+    out, 2-D parts into a 1-D out (also 256 parts of 512 columns: the bias column sums' shape), 30 jobs in
+    one launch; equal to the parts summed one after another within fp32 summation-order rounding, and the
+    same bits on a repeat."""
     from vss_amd.update import sum_parts
     g = torch.Generator(device="cuda").manual_seed(3)
     a = torch.randn(32, 512, 256, device="cuda", generator=g)
@@ -679,6 +682,11 @@ def test_sum_parts_matches_torch_sum_gpu():
     outs = [torch.empty(512, 256, device="cuda"), torch.full((2, 300), 7.0, device="cuda")[:, :256],
             torch.empty(300, device="cuda"), torch.empty(512, device="cuda")]
     jobs = [(a, outs[0]), (b, outs[1]), (c, outs[2]), (d, outs[3])]
+    # and 26 more small jobs: 30 in one launch (the backward of both MLPs queues 18)
+    for k in range(26):
+        p = torch.randn(1 + 9 * k, 3 + k, device="cuda", generator=g)
+        jobs.append((p, torch.empty(3 + k, device="cuda")))
+        outs.append(jobs[-1][1])
     sum_parts(jobs)
     first = [o.clone() for o in outs]
     sum_parts(jobs)

@@ -1192,8 +1192,10 @@ def train(args, on_update=None):
         if args.anneal_lr:
             optimizer.param_groups[0]["lr"] = annealed_lr(update, num_updates, args.learning_rate)
         t_roll = time.time()
-        ep_ret = torch.zeros((), device=device)
-        ep_cnt = torch.zeros((), device=device)
+        # per-env sums of finished episodes' returns and counts, reduced once after the rollout (two
+        # elementwise launches per step instead of a product, two reductions and two adds)
+        ep_ret = torch.zeros(E, device=device)
+        ep_cnt = torch.zeros(E, device=device)
         # ppo…:273-279 logs the first finished env's episode stats at steps 0-2 (a host-sync loop);
         # here: [any done, goal, grad, move, energy, return, length] on the device, read once below
         ep_first = torch.zeros((3, 7), device=device)
@@ -1220,9 +1222,9 @@ def train(args, on_update=None):
             else:
                 with torch.no_grad(), autocast(args, device):
                     next_values[step] = agent.get_value(info["terminal_observation"]).reshape(1, -1)
-            d = next_done.float()
-            ep_ret += (info["r"]["return"] * d).sum()
-            ep_cnt += d.sum()
+            d = next_dones[step]  # next_done as float (the storage row just written)
+            ep_ret.addcmul_(info["r"]["return"].reshape(E), d)
+            ep_cnt.add_(d)
             if step <= 2:
                 ep_first[step] = first_done_stats(d, info)
         if term is not None:
@@ -1252,7 +1254,7 @@ def train(args, on_update=None):
         sps = int(global_step / wall)
         rec = {"update": update, "global_step": global_step, "sps": sps, "wall_s": wall, "rollout_s": t_roll,
                "update_s": t_upd,
-               "episodes": float(ep_cnt), "mean_return": float(ep_ret / ep_cnt.clamp(min=1)),
+               "episodes": float(ep_cnt.sum()), "mean_return": float(ep_ret.sum() / ep_cnt.sum().clamp(min=1)),
                **{k: float(v) for k, v in stats.items()}}
         history.append(rec)
         for k, name in (("v_loss", "value_loss"), ("pg_loss", "policy_loss"), ("entropy", "entropy"),

@@ -375,6 +375,12 @@ int vss_output_backward_direct(void* stream, int64_t rows, int32_t k_out, int32_
  * every VSS wrapper), rows % 64 == 0; grad and x 16-B aligned.  partial (parts, 256, k_in), parts =
  * vss_first_weight_grad_chunks_bf16x6(rows, n_out, k_in) (-1 for a bad shape).  Replaces hipBLASLt's
  * batched grad^T x + torch.sum (the split-K dW of the first layer).
+ *
+ * vss_first_layer_bf16x6: the Agent's FIRST layer forward, y = tanh(x W^T + b) (nn.Linear(obs, 256) +
+ * nn.Tanh, ppo…:131,142) with x (rows, k_in) the observations, w (256, k_in) nn.Linear's weight,
+ * bias (256,), y (rows, 256): n_out == 256, 0 < k_in <= 64, k_in % 4 == 0, any rows >= 0; x and y
+ * 16-B aligned.  The same split products as above (k zero-padded to 64); tanh as the other epilogues.
+ * Replaces the fp32-MFMA first_layer_kernel (vss_linear_tanh) on the update and rollout paths.
  * ------------------------------------------------------------------------------------------- */
 int vss_linear_tanh_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
                            const float* bias, float* y, uint16_t* w_split);
@@ -390,6 +396,8 @@ int vss_weight_planes_bf16x6(void* stream, int32_t count, const float* const* w,
 int64_t vss_weight_grad_chunks_bf16x6(int64_t rows, int32_t n_out, int32_t k_in);
 int vss_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_in, const float* grad, const float* x,
                            float* partial);
+int vss_first_layer_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
+                           const float* bias, float* y);
 int64_t vss_first_weight_grad_chunks_bf16x6(int64_t rows, int32_t n_out, int32_t k_in);
 int vss_first_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int32_t k_in, const float* grad,
                                  const float* x, float* partial);

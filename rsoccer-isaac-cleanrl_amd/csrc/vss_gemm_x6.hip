@@ -914,6 +914,110 @@ static Args fb_args(int32_t k, int32_t n, const uint16_t* w_split, const float* 
   return a;
 }
 
+// ---- the first hidden layer's forward on the bf16 matrix cores: y = tanh(x W^T + b) ---------------------
+// The Agent's first Linear + Tanh (nn.Linear(52, 256), ppo…:131,142) over the update's minibatch and the
+// rollout's observations.  On the fp32 MFMA (vss_update.hip first_layer_kernel) its 56 GFLOP at 2,097,152
+// rows cost 0.46 ms of matrix time before the tanh and the 2.1 GB of stores.  Here each of 8 waves per
+// block takes 16-row slabs on its own: x straight from global memory (lane = row fr, k group fg: two 16-B
+// loads per K step of 32, k >= k_in zero), split into hi / mid / lo in registers (split8); W's three
+// planes were split once per block into LDS as the A fragments ([ks][plane][i tile][fg][fr] x 16 B,
+// 96 KB: a fragment read is 16 consecutive 16-B slots per 16-lane group); per slab 16 i tiles x 2 K
+// steps x 6 products (the x6 order, smallest first), then bias + tanh and 16-B stores of 4 consecutive
+// features of a row.  No barrier after the W split, so one wave's tanh and stores run beside the other
+// waves' MFMAs.  The x6 error bound applies (products exact, the dropped terms < 2^-23 |a||b|).
+constexpr int FL_WAVES = 8, FL_THREADS = 64 * FL_WAVES;
+// Measured at 2,097,152 rows (profiles/r05_first_layer_x6.log): 650-670 us against the fp32-MFMA kernel's
+// 830-870 us; without the stores (timing only) 419 us, without the tanh 648 us -- the HBM stores set it.
+// Not kept, all slower or equal: 16 waves x 128-feature halves (810 us), nontemporal stores (734 us),
+// the stores as whole 128-B lines through a per-wave LDS transpose (653 us), and a branch-free
+// software pipeline that interleaves one slab's tanh / stores with the next slab's MFMAs in every wave
+// (two accumulator sets, buffer-descriptor stores; 670-701 us).
+__global__ __launch_bounds__(FL_THREADS) void first_layer_x6_kernel(int64_t rows, int k, const float* __restrict__ x,
+                                                                    const float* __restrict__ w,
+                                                                    const float* __restrict__ bias,
+                                                                    float* __restrict__ y) {
+  __shared__ u32x4 wimg[2 * 3 * 16 * 64];  // [ks][plane][i tile][fg * 16 + fr]
+  __shared__ float bl[256];
+  for (int p = threadIdx.x; p < 256 * 8; p += FL_THREADS) {  // (feature, k group of 8) pairs
+    const int f = p >> 3, g = p & 7;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int kk = 8 * g + e;
+      v[e] = kk < k ? w[(int64_t)f * k + kk] : 0.0f;
+    }
+    u32x4 pl[3];
+    split8(v, pl[0], pl[1], pl[2]);
+    const int ks = g >> 2, fg = g & 3, it = f >> 4, fr = f & 15;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) wimg[((ks * 3 + q) * 16 + it) * 64 + fg * 16 + fr] = pl[q];
+  }
+  for (int i = threadIdx.x; i < 256; i += FL_THREADS) bl[i] = bias[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, fr = lane & 15, fg = lane >> 4;
+  const int64_t slabs = (rows + 15) / 16, step = (int64_t)gridDim.x * FL_WAVES;
+  auto load_x = [&](int64_t sl, float4 (&xr)[2][2]) __attribute__((always_inline)) {
+    const int64_t row = sl * 16 + fr;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k0 = 32 * ks + 8 * fg + 4 * h;
+        xr[ks][h] = (row < rows && k0 + 4 <= k) ? *reinterpret_cast<const float4*>(x + row * k + k0)
+                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+  };
+  // the six products, smallest first (gemm_x6_kernel's order): lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi
+  constexpr int PP[6] = {2, 0, 1, 1, 0, 0};
+  constexpr int QP[6] = {0, 2, 1, 0, 1, 0};
+  int64_t sl = (int64_t)blockIdx.x * FL_WAVES + wv;
+  float4 xr[2][2];
+  if (sl < slabs) load_x(sl, xr);
+  for (; sl < slabs; sl += step) {
+    u32x4 xp[2][3];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const float v[8] = {xr[ks][0].x, xr[ks][0].y, xr[ks][0].z, xr[ks][0].w,
+                          xr[ks][1].x, xr[ks][1].y, xr[ks][1].z, xr[ks][1].w};
+      split8(v, xp[ks][0], xp[ks][1], xp[ks][2]);
+    }
+    if (sl + step < slabs) load_x(sl + step, xr);  // the next slab's x lands during this one
+    f32x4 acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // 8 steps (group of 4 i tiles, K step); one step's 12 fragments live at a time (without the fences
+    // the compiler hoists all 96 fragment reads of the slab, 384 VGPRs, and spills)
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      const int ig = st >> 1, ks = st & 1;
+      u32x4 pf[3][4];
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) pf[q][ii] = wimg[((ks * 3 + q) * 16 + 4 * ig + ii) * 64 + lane];
+#pragma unroll
+      for (int xx = 0; xx < 6; ++xx)
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+          acc[4 * ig + ii] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pf[PP[xx]][ii]),
+                                                                     __builtin_bit_cast(bf16x8, xp[ks][QP[xx]]),
+                                                                     acc[4 * ig + ii], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int64_t row = sl * 16 + fr;
+    if (row < rows) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int f0 = 16 * i + 4 * fg;
+        f32x4 v = acc[i];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = tanh_f32(v[r] + bl[f0 + r]);
+        *reinterpret_cast<f32x4*>(y + row * 256 + f0) = v;
+      }
+    }
+  }
+}
+
 }  // namespace vx6
 
 extern "C" {
@@ -1042,6 +1146,20 @@ int vss_first_weight_grad_bf16x6(void* stream, int64_t rows, int32_t n_out, int3
   const int g = fw_parts(rows);
   hipLaunchKernelGGL(first_wgrad_kernel, dim3((unsigned)g), dim3(FW_THREADS), 0, (hipStream_t)stream,
                      (int64_t)(rows / (2 * KT)), k_in, grad, x, partial);
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+}
+
+int vss_first_layer_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t n_out, const float* x, const float* w,
+                           const float* bias, float* y) {
+  using namespace vx6;
+  if (rows < 0 || n_out != 256 || k_in <= 0 || k_in > 64 || k_in % 4 != 0 || misaligned(x) || !w || !bias ||
+      misaligned(y))
+    return VSS_E_ARG;
+  if (rows == 0) return VSS_OK;
+  int64_t g = ((rows + 15) / 16 + FL_WAVES - 1) / FL_WAVES;
+  if (g > 256) g = 256;  // one block per CU (96 KB of W planes), persistent over the slabs
+  hipLaunchKernelGGL(first_layer_x6_kernel, dim3((unsigned)g), dim3(FL_THREADS), 0, (hipStream_t)stream, rows, k_in, x,
+                     w, bias, y);
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 

@@ -42,7 +42,8 @@ EXPORTED = ("vss_abi_version", "vss_source_hash", "vss_error_string", "vss_step"
             "vss_first_weight_grad_bf16x6", "vss_weight_planes_bf16x6", "vss_ppo_loss_scratch_floats", "vss_ppo_loss",
             "vss_grad_sq_partials_count", "vss_grad_sq_partials", "vss_adam_step_clipped", "vss_sum_parts",
             "vss_output_backward_direct_chunks", "vss_output_backward_direct", "vss_ppo_loss_direct_scratch_floats",
-            "vss_ppo_loss_direct", "vss_minibatch_gather_parts", "vss_minibatch_gather", "vss_adv_part_sum")
+            "vss_ppo_loss_direct", "vss_minibatch_gather_parts", "vss_minibatch_gather", "vss_adv_part_sum",
+            "vss_first_layer_bf16x6")
 
 
 class VssParams(ctypes.Structure):
@@ -211,6 +212,8 @@ def load() -> ctypes.CDLL:
     L.vss_minibatch_gather.restype = ctypes.c_int
     L.vss_adv_part_sum.argtypes = [P, i32, P, P]
     L.vss_adv_part_sum.restype = ctypes.c_int
+    L.vss_first_layer_bf16x6.argtypes = [P, i64, i32, i32, P, P, P, P]
+    L.vss_first_layer_bf16x6.restype = ctypes.c_int
     if L.vss_abi_version() != ABI_VERSION:
         raise NativeError(f"libvss_amd ABI {L.vss_abi_version()} != expected {ABI_VERSION}")
     _lib = L

@@ -413,6 +413,24 @@ def weight_grad_x6(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None
     return _reduce_parts(parts, out, defer)
 
 
+def first_layer_x6_ok(k: int, n: int) -> bool:
+    """Shapes vss_first_layer_bf16x6 takes (the Agent's first layer): n 256, k <= 64 and k % 4 == 0."""
+    return n == 256 and 0 < k <= 64 and k % 4 == 0
+
+
+def first_layer_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """tanh(x @ w.T + b) for the Agent's first layer (x (rows, k <= 64) the observations, w (256, k)) on the
+    bf16 matrix cores with fp32 arithmetic (vss_first_layer_bf16x6), any row count."""
+    rows, k = x.shape
+    n = w.shape[0]
+    _x6_check("vss_first_layer_bf16x6", w.shape == (n, k) and b.shape == (n,) and first_layer_x6_ok(k, n), x, w, b)
+    x, w, b = x.contiguous(), w.contiguous(), b.contiguous()
+    y = _out(out, (rows, n), x)
+    N.check(N.load().vss_first_layer_bf16x6(N.stream_of(x.device), rows, k, n, x.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                            y.data_ptr()), "vss_first_layer_bf16x6")
+    return y
+
+
 def first_wgrad_ok(rows: int, n_out: int, k_in: int) -> bool:
     """Shapes vss_first_weight_grad_bf16x6 takes (the Agent's first layer): n_out 256, k_in <= 64 and
     k_in % 4 == 0, rows % 64."""
@@ -446,6 +464,8 @@ def first_weight_grad_x6(grad: torch.Tensor, x: torch.Tensor, out: torch.Tensor 
 def linear_tanh_mixed(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, planes: torch.Tensor | None = None) -> torch.Tensor:
     rows, k = x.shape
     n = w.shape[0]
+    if x.is_cuda and rows > 0 and first_layer_x6_ok(k, n):
+        return first_layer_x6(x, w, b)  # the first layer (52 -> 256): every row on the bf16 matrix cores
     main = rows // 256 * 256
     if main == 0 or not x6_ok(main, k, n):
         return linear_tanh(x, w, b)

@@ -8,7 +8,8 @@ import pytest
 import torch
 
 from vss_amd import _native as N
-from vss_amd.update import (first_weight_grad_x6, first_wgrad_ok, linear_tanh, linear_tanh_backward,
+from vss_amd.update import (first_layer_x6, first_layer_x6_ok, first_weight_grad_x6, first_wgrad_ok, linear_tanh,
+                            linear_tanh_backward,
                             linear_tanh_backward_mixed, linear_tanh_backward_x6,
                             linear_tanh_mixed, linear_tanh_out_mixed, linear_tanh_out_x6, linear_tanh_x6,
                             weight_grad_mixed, weight_grad_x6, x6_ok, x6_wgrad_ok)
@@ -138,6 +139,69 @@ def test_x6_first_layer_weight_grad_exact_and_per_product_gpu():
     big = torch.randn(2 * rows, 52, device="cuda", generator=g)
     gz = torch.randn(rows, 256, device="cuda", generator=g)
     assert torch.equal(first_weight_grad_x6(gz, big[::2]), first_weight_grad_x6(gz, big[::2].contiguous()))
+
+
+def test_first_layer_x6_shape_predicate_cpu():
+    """The first layer's forward (nn.Linear(52, 256) + Tanh): n 256, k <= 64 and % 4, any rows."""
+    assert first_layer_x6_ok(52, 256) and first_layer_x6_ok(4, 256) and first_layer_x6_ok(64, 256)
+    assert not first_layer_x6_ok(68, 256) and not first_layer_x6_ok(50, 256) and not first_layer_x6_ok(52, 512)
+    with pytest.raises(ValueError):
+        first_layer_x6(torch.zeros(16, 52), torch.zeros(256, 52), torch.zeros(256))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k_in", [52, 4, 64, 36])
+@pytest.mark.parametrize("rows", [1, 17, 4096 + 5, 131040, 2097152])
+def test_x6_first_layer_forward_error_at_most_fp32_gpu(rows, k_in):
+    """The first layer's y = tanh(x W^T + b) on vss_first_layer_bf16x6 (x the observations, any row
+    count): error vs fp64 no larger than the fp32-MFMA first_layer_kernel's (vss_linear_tanh, the
+    kernel it replaces, with the same tanh_f32; x 1.25 slack), below 4e-6 of max|y|; two calls give the
+    same bits.  (hipBLASLt's addmm + torch's tanh is printed beside: at small k its error is torch's
+    correctly rounded tanh, not the GEMM.)"""
+    g = torch.Generator(device="cuda").manual_seed(rows + k_in)
+    x = torch.randn(rows, k_in, device="cuda", generator=g) * 1.5
+    w = torch.randn(256, k_in, device="cuda", generator=g) * (2.0 / k_in) ** 0.5
+    b = torch.randn(256, device="cuda", generator=g) * 0.1
+    n = min(rows, 65536)
+    ref = torch.tanh(x[:n].double() @ w.double().t() + b.double())
+    got = first_layer_x6(x, w, b)
+    assert got.shape == (rows, 256)
+    e6 = _rel(got[:n], ref)
+    ef = _rel(linear_tanh(x, w, b)[:n], ref)
+    et = _rel(torch.addmm(b, x[:n], w.t()).tanh_(), ref)
+    assert e6[0] < 4e-6 and e6[1] < 1.25 * ef[1] + 1e-8, (e6, ef, et)
+    assert torch.equal(got, first_layer_x6(x, w, b))
+
+
+@pytest.mark.gpu
+def test_x6_first_layer_forward_exact_and_in_the_update_gpu():
+    """Integer operands with exact fp32 sums: the same bits as the fp32-MFMA kernel (both take tanh_f32
+    of the exact pre-activation); a strided minibatch view gives the contiguous copy's bits; and
+    linear_tanh_mixed (the update's and the rollout chain's first layer) runs this kernel."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    rows = 4096 + 3
+    xi = torch.randint(-3, 4, (rows, 52), device="cuda", generator=g).float()
+    wi = torch.randint(-2, 3, (256, 52), device="cuda", generator=g).float() / 64
+    bi = torch.randint(-8, 9, (256,), device="cuda", generator=g).float() / 16
+    assert torch.equal(first_layer_x6(xi, wi, bi), linear_tanh(xi, wi, bi))
+    big = torch.randn(2 * rows, 52, device="cuda", generator=g)
+    w = torch.randn(256, 52, device="cuda", generator=g) * 0.2
+    b = torch.randn(256, device="cuda", generator=g) * 0.1
+    assert torch.equal(first_layer_x6(big[::2], w, b), first_layer_x6(big[::2].contiguous(), w, b))
+    assert torch.equal(linear_tanh_mixed(big[:rows], w, b), first_layer_x6(big[:rows], w, b))
+
+
+@pytest.mark.gpu
+def test_x6_first_layer_forward_refusals_gpu():
+    lib = N.load()
+    buf = torch.zeros(1 << 20, device="cuda")
+    p, s = buf.data_ptr(), N.stream_of(buf.device)
+    assert lib.vss_first_layer_bf16x6(s, 64, 68, 256, p, p, p, p) != 0  # k_in > 64
+    assert lib.vss_first_layer_bf16x6(s, 64, 50, 256, p, p, p, p) != 0  # k_in % 4
+    assert lib.vss_first_layer_bf16x6(s, 64, 52, 512, p, p, p, p) != 0  # n_out != 256
+    assert lib.vss_first_layer_bf16x6(s, 64, 52, 256, p + 4, p, p, p) != 0  # misaligned x
+    assert lib.vss_first_layer_bf16x6(s, 64, 52, 256, p, p, p, p + 4) != 0  # misaligned y
+    assert lib.vss_first_layer_bf16x6(s, 0, 52, 256, p, p, p, p) == 0
 
 
 @pytest.mark.gpu

@@ -355,7 +355,7 @@ int vss_output_backward_direct(void* stream, int64_t rows, int32_t k_out, int32_
  * w (resp. w_next_t) == NULL: w_split already holds the weight's planes, written by
  * vss_weight_planes_bf16x6 for this (n_out, k) since the weight last changed (no split launch).
  *
- * vss_weight_planes_bf16x6: the planes of `count` (1..8) weights in ONE launch, into the w_split
+ * vss_weight_planes_bf16x6: the planes of `count` (1..16) weights in ONE launch, into the w_split
  * buffers the GEMM entries above then take with a NULL weight: job q is an (n[q], k[q]) operand
  * (n % 128 == 0, n <= 4096, k % 64 == 0), stored row-major as w[q] (n, k) when transpose[q] == 0, or
  * as its transpose (k, n) when transpose[q] == 1 (the backward's W_next^T straight from nn.Linear's

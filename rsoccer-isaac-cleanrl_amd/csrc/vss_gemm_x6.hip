@@ -306,7 +306,7 @@ struct PlaneJob {
   int64_t n, k;
   int32_t trans, r;
 };
-constexpr int kMaxPlaneJobs = 8;
+constexpr int kMaxPlaneJobs = 16;  // both MLPs of the Agent: 2 x 6
 struct PlaneJobs {
   PlaneJob j[kMaxPlaneJobs];
 };

@@ -301,21 +301,28 @@ def _mlp_planes(ws, rows: int):
     launch): {layer: planes of W} for the forwards of layers 1 .. L-2 and {layer: planes of W^T} for
     their backwards (layer 0's input width is the observation's, below the x6 shapes; layer L-1 is the
     output layer).  Valid for this minibatch: the weights change only at the optimizer step."""
+    return _nets_planes([ws], rows)[0]
+
+
+def _nets_planes(nets, rows: int):
+    """_mlp_planes for several MLPs (nets = [their weight lists]) in one launch while the jobs fit it."""
     if rows < 256:
-        return {}, {}
+        return [({}, {}) for _ in nets]
     jobs = []
-    for layer in range(1, len(ws) - 1):
-        n, k = ws[layer].shape
-        if x6_ok(256, k, n):
-            jobs.append((layer, False))
-        if x6_ok(256, n, k):
-            jobs.append((layer, True))
-    if not jobs:
-        return {}, {}
-    planes = weight_planes([(ws[layer], tr) for layer, tr in jobs])
-    pf = {layer: p for (layer, tr), p in zip(jobs, planes) if not tr}
-    pb = {layer: p for (layer, tr), p in zip(jobs, planes) if tr}
-    return pf, pb
+    for q, ws in enumerate(nets):
+        for layer in range(1, len(ws) - 1):
+            n, k = ws[layer].shape
+            if x6_ok(256, k, n):
+                jobs.append((q, layer, False))
+            if x6_ok(256, n, k):
+                jobs.append((q, layer, True))
+    out = [({}, {}) for _ in nets]
+    for j0 in range(0, len(jobs), 16):
+        chunk = jobs[j0:j0 + 16]
+        planes = weight_planes([(nets[q][layer], tr) for q, layer, tr in chunk])
+        for (q, layer, tr), p in zip(chunk, planes):
+            out[q][1 if tr else 0][layer] = p
+    return out
 
 
 # the fused path's GEMM arithmetic: "x6" (default) = fp32 products on the bf16 matrix cores from an
@@ -728,9 +735,12 @@ def direct_minibatch(agent, args, obs, act, logp, adv, adv_part, adv_count, ret,
     (rows_pad rows, the padding repeating the minibatch), logp / adv / ret / val (rows); adv RAW, normalised
     inside the loss from adv_part / adv_count (vss_ppo_loss_direct; None: as given).  Returns (loss,
     (pg_loss, v_loss, entropy_loss, old_approx_kl, approx_kl, clipfrac))."""
+    (pfa, pba), (pfc, pbc) = _nets_planes([_mlp_wb(agent.actor_mean)[0], _mlp_wb(agent.critic)[0]], obs.shape[0])
+    planes = {id(agent.actor_mean): (pfa, pba), id(agent.critic): (pfc, pbc)}
+
     def forward(seq):
         ws, bs = _mlp_wb(seq)
-        pf, pb = _mlp_planes(ws, obs.shape[0])
+        pf, pb = planes[id(seq)]
         hs = [obs]
         for layer in range(len(ws) - 2):
             hs.append(linear_tanh_mixed(hs[-1], ws[layer], bs[layer], planes=pf.get(layer)))

@@ -289,10 +289,10 @@ def weight_planes(jobs) -> list:
     """The bf16 planes of several weights in ONE launch (vss_weight_planes_bf16x6): jobs = [(w, transpose)]
     with w an fp32 (n, k) weight (transpose False: the forward's P operand) or a (k, n) one whose
     transpose is the operand (True: the backward's W_next^T, no transposed copy); at most 8.  Returns
-    the planes, to be handed to linear_tanh_x6 / linear_tanh_out_x6 / linear_tanh_backward_x6 (planes=),
+    the planes (at most 16 jobs), to be handed to linear_tanh_x6 / linear_tanh_out_x6 / linear_tanh_backward_x6 (planes=),
     valid until the weights change."""
-    if not 1 <= len(jobs) <= 8:
-        raise ValueError(f"weight_planes: 1..8 weights per launch, got {len(jobs)}")
+    if not 1 <= len(jobs) <= 16:
+        raise ValueError(f"weight_planes: 1..16 weights per launch, got {len(jobs)}")
     ws, ns, ks, ts, outs = [], [], [], [], []
     for w, tr in jobs:
         if w.dim() != 2 or w.dtype != torch.float32 or not w.is_cuda or not w.is_contiguous():

@@ -409,7 +409,7 @@ def test_weight_planes_refusals_gpu():
     with pytest.raises(ValueError):
         weight_planes([])
     with pytest.raises(ValueError):
-        weight_planes([(w, False)] * 9)
+        weight_planes([(w, False)] * 17)  # at most 16 per launch
     with pytest.raises(N.NativeError):
         weight_planes([(torch.randn(100, 512, device="cuda"), False)])  # n % 128
     with pytest.raises(N.NativeError):

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Profiling-only: the update's forward / backward x6 shapes at ROWS rows (default 2,097,152), timed
-with HIP events over REPS launches each, in the kernel variant the environment selects (VSS_X6_PP=0:
-gemm_x6_kernel's 256 x 128 block; default: gemm_pp_kernel with VSS_X6_PE epilogue steps).  Prints
+"""Profiling-only: the update's forward / backward / weight-gradient x6 shapes at ROWS rows (default
+2,097,152), timed with HIP events over REPS launches each, in the kernel variant the environment selects
+(round 5: VSS_X6_PRIO=1 raises the second half of each block's waves to s_setprio 1).  Prints
 fp32-equivalent TF per shape and a checksum of each output (compare runs for the same bits)."""
 import os
 import sys
@@ -10,11 +10,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "rsoccer-isaac-cleanrl_amd"))
 import torch  # noqa: E402
 
-from vss_amd.update import linear_tanh_backward_x6, linear_tanh_out_x6, linear_tanh_x6  # noqa: E402
+from vss_amd.update import linear_tanh_backward_x6, linear_tanh_out_x6, linear_tanh_x6, weight_grad_x6  # noqa: E402
 
 rows = int(os.environ.get("ROWS", 2097152))
 reps = int(os.environ.get("REPS", 10))
-tag = f"PP={os.environ.get('VSS_X6_PP', '1')} PE={os.environ.get('VSS_X6_PE', '2')}"
+tag = f"PRIO={os.environ.get('VSS_X6_PRIO', '0')}"
 g = torch.Generator(device="cuda").manual_seed(0)
 
 
@@ -57,5 +57,8 @@ for k, n in ((256, 512), (512, 512), (512, 256)):
     ms = timed(lambda: res.update(o=linear_tanh_backward_x6(gn, wn, yk, out=gz)))
     print(f"{tag} backward {k}<-{n}: {ms:.3f} ms {2 * rows * k * n / ms / 1e9:.1f} TF  sum {csum(gz)} db {csum(res['o'][1])}",
           flush=True)
+    res = {}
+    ms = timed(lambda: res.update(o=weight_grad_x6(gn, yk)))
+    print(f"{tag} wgrad {n}x{k}: {ms:.3f} ms {2 * rows * k * n / ms / 1e9:.1f} TF  sum {csum(res['o'])}", flush=True)
     del gn, yk, gz
     torch.cuda.empty_cache()

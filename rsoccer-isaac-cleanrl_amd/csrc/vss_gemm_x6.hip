@@ -36,7 +36,6 @@
 // XCD-aware slot map of vss_update.hip (the i tiles of a row band run together on one XCD).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 #include <type_traits>
 
@@ -180,7 +179,6 @@ struct Args {
   float* partial;          // EPI_DTANH: (grid / ni, I) column sums of out
   const float* w_out;      // EPI_TANH_OUT: (KO, I)
   float* out_part;         // EPI_TANH_OUT: (I / 64, J, KO)
-  int32_t prio;            // A/B (this round's measurement): waves of the block's second half at s_setprio 1
 };
 
 // one thread's register-staged operands of one K tile: NP groups of 8 raw fp32 values
@@ -375,7 +373,6 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
   const int G = gridDim.x;
   const int slot = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   if (slot >= a.items) return;
-  if (a.prio && __builtin_amdgcn_readfirstlane(wv) >= C::THREADS / 128) __builtin_amdgcn_s_setprio(1);
   const int per_split = a.ni * a.nj;
 
   // work item w -> (split, j tile, i tile); j-band major so the ni i tiles of a band are consecutive
@@ -881,17 +878,8 @@ static Plan wg_plan(int64_t rows, int32_t n_out, int32_t k_in) {
   return p;
 }
 
-static int x6_prio() {
-  static const int v = [] {
-    const char* e = getenv("VSS_X6_PRIO");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return v;
-}
-
 template <int EPI, int SP, int SQ, class C, int KO = 0>
 static int launch(void* stream, Args a, const Plan& pl) {
-  a.prio = x6_prio();
   a.ni = pl.ni;
   a.nj = pl.nj;
   a.kpairs = pl.kpairs;

@@ -391,6 +391,26 @@ int64_t vss_linear_tanh_backward_chunks_bf16x6(int64_t rows, int32_t k_next, int
 int vss_linear_tanh_backward_bf16x6(void* stream, int64_t rows, int32_t k_next, int32_t n_out, const float* grad_next,
                                     const float* w_next_t, const float* y, float* grad_in, float* bias_partial,
                                     uint16_t* w_split);
+/* vss_linear_tanh_loss_bf16x6: the last hidden layer, the output layer, the minibatch's PPO loss terms and
+ * the output layer's backward in ONE x6 launch (direct_minibatch): y = tanh(x W^T + b) stays in the
+ * accumulators, out = y w_out^T + b_out, each row's loss terms and gradient g_out as vss_ppo_loss_direct
+ * forms them (role 0: the actor's policy terms, k_out in {1, 2}, advantages normalised from adv_part as
+ * there; role 1: the critic's value terms, k_out == 1), and grad_in (rows_pad, 256) = (g_out w_out)
+ * (1 - y^2) -- the hidden layer's pre-activation gradient, written instead of y.  Rows >= rows are
+ * padding: zero gradient, no loss term.  Per block b of vss_linear_tanh_loss_blocks_bf16x6(rows_pad, k_in,
+ * n_out) (-1 for a bad shape): part_cs[b] (256,) its column sums of grad_in (the hidden bias gradient),
+ * part_dwo[b] (k_out, 256) its g_out^T y (the output weight gradient), part_stats[b] (32,) its loss sums
+ * (csrc/vss_loss_row.h kBlockStats) for vss_ppo_loss_fused_finish.  n_out == 256, rows_pad % 256 == 0,
+ * k_in % 64 == 0; w_split the weight's bf16 planes (vss_weight_planes_bf16x6), x / grad_in 16-B aligned.
+ * Replaces vss_linear_tanh_out_bf16x6 + vss_ppo_loss_direct's row pass + vss_output_backward_direct. */
+int64_t vss_linear_tanh_loss_blocks_bf16x6(int64_t rows, int32_t k_in, int32_t n_out);
+int vss_linear_tanh_loss_bf16x6(void* stream, int32_t role, int64_t rows_pad, int64_t rows, int32_t k_in, int32_t n_out,
+                                const float* x, const float* bias, int32_t k_out, const float* w_out, const float* b_out,
+                                const float* action, const float* logprob_old, const float* adv, const double* adv_part,
+                                int32_t adv_nparts, double adv_count, const float* logstd, const float* returns,
+                                const float* values_old, float clip_coef, float clip_lo, float clip_hi, float vf_coef,
+                                int32_t clip_vloss, float* grad_in, float* part_cs, float* part_dwo, float* part_stats,
+                                const uint16_t* w_split);
 int vss_weight_planes_bf16x6(void* stream, int32_t count, const float* const* w, const int32_t* n, const int32_t* k,
                              const int32_t* transpose, uint16_t* const* w_split);
 int64_t vss_weight_grad_chunks_bf16x6(int64_t rows, int32_t n_out, int32_t k_in);
@@ -455,6 +475,13 @@ int vss_ppo_loss_direct(void* stream, int64_t rows, int64_t rows_pad, int32_t n_
                         float ent_coef, float vf_coef, int32_t clip_vloss, float* grad_mean, float* grad_value,
                         float* grad_logstd, float* grad_mean_bias, float* grad_value_bias, float* loss_out,
                         float* stats_out, float* partial);
+/* vss_ppo_loss_fused_finish: vss_linear_tanh_loss_bf16x6's per-block loss sums of the actor (actor_blocks)
+ * and the critic (critic_blocks) -> loss_out[1], stats_out[6], grad_logstd, grad_mean_bias (n_act,) and
+ * grad_value_bias (1,) as vss_ppo_loss_direct writes them; n_act in {1, 2}. */
+int vss_ppo_loss_fused_finish(void* stream, int64_t rows, int32_t n_act, int64_t actor_blocks, const float* actor_stats,
+                              int64_t critic_blocks, const float* critic_stats, const float* logstd, float ent_coef,
+                              float vf_coef, float* grad_logstd, float* grad_mean_bias, float* grad_value_bias,
+                              float* loss_out, float* stats_out);
 int64_t vss_minibatch_gather_parts(int64_t mb);
 int vss_minibatch_gather(void* stream, int64_t mb, int64_t rows_pad, int64_t batch, const int64_t* inds, int64_t obs_w,
                          int64_t act_w, const float* b_obs, const float* b_act, const float* b_logp, const float* b_adv,

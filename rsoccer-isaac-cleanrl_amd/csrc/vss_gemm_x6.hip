@@ -40,6 +40,7 @@
 #include <type_traits>
 
 #include "../../include/vss.h"
+#include "vss_loss_row.h"
 
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
 #error "vss_gemm_x6.hip targets gfx950 (CDNA4) only: v_mfma_f32_16x16x32_bf16, v_cvt_pk_bf16_f32"
@@ -55,7 +56,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 
-enum { EPI_TANH = 0, EPI_DTANH = 1, EPI_TANH_OUT = 2, EPI_WGRAD = 3 };
+enum { EPI_TANH = 0, EPI_DTANH = 1, EPI_TANH_OUT = 2, EPI_WGRAD = 3, EPI_LOSS_A = 4, EPI_LOSS_C = 5 };
 enum { ST_ROW = 0, ST_TR = 1, ST_DMA = 2, ST_TR2 = 3, ST_KROW = 4 };
 
 constexpr int KT = 32;  // K tile = one v_mfma_f32_16x16x32_bf16 step
@@ -177,9 +178,31 @@ struct Args {
   const float* bias;       // EPI_TANH*: (I)
   const float* y;          // EPI_DTANH: (J, I) the tanh output the gradient passes through
   float* partial;          // EPI_DTANH: (grid / ni, I) column sums of out
-  const float* w_out;      // EPI_TANH_OUT: (KO, I)
+  const float* w_out;      // EPI_TANH_OUT / EPI_LOSS_*: (KO, I)
   float* out_part;         // EPI_TANH_OUT: (I / 64, J, KO)
+  // EPI_LOSS_A / EPI_LOSS_C: the last hidden layer, the output layer and the minibatch loss of
+  // ppo…:318-349 (the actor's policy terms / the critic's value terms) folded into one epilogue; out receives
+  // the hidden layer's pre-activation gradient gz = (g_out W_out) (1 - y^2), never y
+  const float* b_out;      // (KO) the output layer's bias
+  const float* l_act;      // actor: the actions (rows, KO)
+  const float* l_logp;     // actor: the rollout log-probs (rows)
+  const float* l_adv;      // actor: the RAW advantages (rows), normalised from adv_part when given
+  const double* adv_part;  // actor: (adv_nparts, 2) fp64 (sum, sum of squares) parts, or NULL
+  int32_t adv_nparts;
+  double adv_count;
+  const float* logstd;     // actor: (KO)
+  const float* l_ret;      // critic: returns (rows)
+  const float* l_val;      // critic: rollout values (rows), read with clip_vloss
+  float clip, clip_lo, clip_hi, vf_coef, inv_n;
+  int32_t clip_vloss;
+  int64_t rows_real;       // rows of the minibatch (the rest are padding: zero gradient, no loss term)
+  float* part_cs;          // (grid, I) the block's column sums of gz (the hidden layer's bias gradient)
+  float* part_dwo;         // (grid, KO, I) the block's g_out^T y (the output layer's weight gradient)
+  float* part_stats;       // (grid, 32) the block's loss sums (kLossStats layout)
 };
+
+// EPI_LOSS_*: per-block loss sums (vss_loss_row.h kBlockStats layout)
+constexpr int kLossStats = vlossrow::kBlockStats;
 
 // one thread's register-staged operands of one K tile: NP groups of 8 raw fp32 values
 template <int NP>
@@ -364,7 +387,15 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
   constexpr int NQ = Img<BI>::BYTES / (C::THREADS / 64) / 1024;  // 1-KB DMA slices per wave per K tile
   static_assert(!PDMA || NQ * (C::THREADS / 64) * 1024 == Img<BI>::BYTES, "DMA slices: whole KB per wave");
   // EPI_DTANH: (WJ, BI) column sums, accumulated item by item
-  constexpr int EPI_FLOATS = EPI == EPI_TANH_OUT ? KO * 256 + BI : (EPI == EPI_WGRAD ? 1 : (EPI == EPI_DTANH ? C::WJ * BI : BI));
+  constexpr bool LOSS = EPI == EPI_LOSS_A || EPI == EPI_LOSS_C;
+  // EPI_LOSS_*: bias | W_out | the output parts / row gradients (WI x BJ x KO) | column sums (WJ x BI) |
+  // g_out^T y (WJ x KO x BI) | loss sums of waves 0, 1 (2 x 32) | advantage mean, std
+  constexpr int E_P = BI + KO * 256, E_CS = E_P + C::WI * BJ * KO, E_DW = E_CS + C::WJ * BI,
+                E_ST = E_DW + C::WJ * KO * BI, E_AD = E_ST + 2 * kLossStats;
+  constexpr int EPI_FLOATS = LOSS ? E_AD + 2
+                                  : (EPI == EPI_TANH_OUT ? KO * 256 + BI
+                                                         : (EPI == EPI_WGRAD ? 1 : (EPI == EPI_DTANH ? C::WJ * BI : BI)));
+  static_assert(!LOSS || (BI == 256 && KO >= 1 && KO <= 2), "EPI_LOSS_*: whole 256-feature rows, 1 or 2 outputs");
   // one LDS object (a second __shared__ array beside a global_load_lds target can make hipcc wait
   // vmcnt(0) before the k-steps' LDS reads, cdna_hip_programming.md §5)
   __shared__ __attribute__((aligned(16))) char lds[C::LDS + EPI_FLOATS * 4];
@@ -389,8 +420,31 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
   if constexpr (EPI != EPI_WGRAD) {
     for (int i = tid; i < (EPI == EPI_DTANH ? EPI_FLOATS : BI); i += C::THREADS)
       epi_lds[i] = EPI == EPI_DTANH ? 0.f : a.bias[it0 * BI + i];
-    if constexpr (EPI == EPI_TANH_OUT)
+    if constexpr (EPI == EPI_TANH_OUT || LOSS)
       for (int i = tid; i < KO * 256; i += C::THREADS) epi_lds[BI + i] = a.w_out[i];
+    if constexpr (LOSS) {
+      for (int i = E_CS + tid; i < E_AD; i += C::THREADS) epi_lds[i] = 0.f;
+      if (EPI == EPI_LOSS_A && a.adv_part && wv == 0) {
+        // the advantages' mean and std from the fp64 parts (vss_loss.hip adv_moments' order)
+        double s0 = 0.0, q0 = 0.0;
+        for (int i = lane; i < a.adv_nparts; i += 64) {
+          s0 += a.adv_part[2 * i];
+          q0 += a.adv_part[2 * i + 1];
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+          s0 += __shfl_xor(s0, m);
+          q0 += __shfl_xor(q0, m);
+        }
+        if (lane == 0) {
+          const double n = a.adv_count, m = s0 / n;
+          double var = (q0 - n * m * m) / (n - 1.0);
+          var = var > 0.0 ? var : 0.0;
+          epi_lds[E_AD] = (float)m;
+          epi_lds[E_AD + 1] = (float)sqrt(var);
+        }
+      }
+    }
   }
 
   // fetch cursor over the flat sequence of (item, k tile)
@@ -500,6 +554,141 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
                                                               __builtin_bit_cast(bf16x8, qf[QP[x]][j]), acc[i][j], 0, 0, 0);
   };
 
+  // EPI_LOSS_*: the item's epilogue in three phases separated by barriers.  (1) y = tanh(acc + b) kept in
+  // the accumulators, the wave's 64-feature slice of each row's output-layer sums into LDS; (2) one thread
+  // per row: the output (4 slices in order, then the bias), that row's loss terms and its gradient g_out
+  // (zero for padding rows), the terms summed per wave into LDS; (3) every lane: gz = (g_out W_out)
+  // (1 - y^2) stored for its rows and features, and the item's column sums of gz and g_out^T y added to
+  // per-(wave row, feature) slots (one lane per slot).
+  auto loss_epilogue = [&](f32x4 (&ac)[TI][TJ], int it, int jt) __attribute__((always_inline)) {
+    if constexpr (LOSS) {
+      const int ib = it * BI + wi * C::WTI;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int rl = wj * C::WTJ + 16 * j + fr;  // row within the item
+        float od[KO];
+#pragma unroll
+        for (int o = 0; o < KO; ++o) od[o] = 0.f;
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int il = wi * C::WTI + 16 * i + 4 * fg;
+          f32x4 v = ac[i][j];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = tanh_f32(v[r] + epi_lds[il + r]);
+          ac[i][j] = v;
+#pragma unroll
+          for (int o = 0; o < KO; ++o) {
+            const float* wo = epi_lds + BI + o * 256 + ib + 16 * i + 4 * fg;
+            float d = v[0] * wo[0];
+            d = fmaf(v[1], wo[1], d);
+            d = fmaf(v[2], wo[2], d);
+            d = fmaf(v[3], wo[3], d);
+            od[o] += d;
+          }
+        }
+#pragma unroll
+        for (int o = 0; o < KO; ++o) {
+          float d = od[o];
+          d += __shfl_xor(d, 16);
+          d += __shfl_xor(d, 32);
+          if (fg == 0) epi_lds[E_P + (wi * BJ + rl) * KO + o] = d;
+        }
+      }
+      __syncthreads();
+      if (tid < BJ) {  // waves 0 and 1 whole: one thread per row of the item
+        const int64_t grow = (int64_t)jt * BJ + tid;
+        float outv[KO], g[KO], t[kLossStats > 0 ? 5 + 2 * KO : 1];
+#pragma unroll
+        for (int o = 0; o < KO; ++o) {
+          float d = epi_lds[E_P + tid * KO + o];
+#pragma unroll
+          for (int q = 1; q < C::WI; ++q) d += epi_lds[E_P + (q * BJ + tid) * KO + o];
+          outv[o] = d + a.b_out[o];
+          g[o] = 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 5 + 2 * KO; ++k) t[k] = 0.f;
+        if (grow < a.rows_real) {
+          if constexpr (EPI == EPI_LOSS_A) {
+            float var[KO], lsc[KO], x[KO], gm[KO], lg[KO];
+            vlossrow::actor_consts<KO>(a.logstd, var, lsc);
+#pragma unroll
+            for (int o = 0; o < KO; ++o) x[o] = a.l_act[grow * KO + o];
+            float A = a.l_adv[grow];
+            if (a.adv_part) A = (A - epi_lds[E_AD]) / (epi_lds[E_AD + 1] + 1e-8f);
+            vlossrow::actor_row<KO>(outv, x, a.l_logp[grow], A, var, lsc, a.clip, a.clip_lo, a.clip_hi, a.inv_n, t[0],
+                                    t[2], t[3], t[4], gm, lg);
+#pragma unroll
+            for (int o = 0; o < KO; ++o) {
+              g[o] = gm[o];
+              t[5 + o] = lg[o];
+              t[5 + KO + o] = gm[o];
+            }
+          } else {
+            float gv;
+            vlossrow::critic_row(outv[0], a.l_ret[grow], a.clip_vloss ? a.l_val[grow] : 0.f, a.clip_vloss, a.clip,
+                                 a.vf_coef, a.inv_n, t[1], gv);
+            g[0] = gv;
+            t[5] = gv;
+          }
+        }
+        // the row gradient over this row's first output part (read above by this thread only)
+#pragma unroll
+        for (int o = 0; o < KO; ++o) epi_lds[E_P + tid * KO + o] = g[o];
+#pragma unroll
+        for (int k = 0; k < 5 + 2 * KO; ++k) {
+          float v = t[k];
+#pragma unroll
+          for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+          if (lane == 0) epi_lds[E_ST + wv * kLossStats + k] += v;
+        }
+      }
+      __syncthreads();
+      // feature group by feature group (i outer): 4 + 4 KO sums live, not TI times that
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int il = wi * C::WTI + 16 * i + 4 * fg;
+        float cs[4] = {0.f, 0.f, 0.f, 0.f}, dw[4][KO];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int o = 0; o < KO; ++o) dw[r][o] = 0.f;
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int rl = wj * C::WTJ + 16 * j + fr;
+          const int64_t jg = (int64_t)jt * BJ + rl;
+          float g[KO];
+#pragma unroll
+          for (int o = 0; o < KO; ++o) g[o] = epi_lds[E_P + rl * KO + o];
+          const f32x4 v = ac[i][j];
+          vx6::f32x4 z;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float sg = g[0] * epi_lds[BI + il + r];
+#pragma unroll
+            for (int o = 1; o < KO; ++o) sg = fmaf(g[o], epi_lds[BI + o * 256 + il + r], sg);
+            z[r] = sg * fmaf(-v[r], v[r], 1.0f);
+            cs[r] += z[r];
+#pragma unroll
+            for (int o = 0; o < KO; ++o) dw[r][o] = fmaf(g[o], v[r], dw[r][o]);
+          }
+          __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ib + 16 * i + 4 * fg));
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = il + r;
+          const float tc = row16_sum(cs[r]);
+          if (fr == 0) epi_lds[E_CS + wj * BI + f] += tc;
+#pragma unroll
+          for (int o = 0; o < KO; ++o) {
+            const float td = row16_sum(dw[r][o]);
+            if (fr == 0) epi_lds[E_DW + (wj * KO + o) * BI + f] += td;
+          }
+        }
+      }
+    }
+  };
+
   Stage<PI + PJ> r0, r1;
   gload(r0);  // K tile 0
   dma_p(0, 0);
@@ -559,6 +748,12 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     // latencies overlap one another and that work instead of adding up group by group (the K loop's
     // registers are free here); backward 8-13 % faster than one load per group at its use would be
     // without any y traffic (tools/x6_ablate.py noy, profiles/r03z_epi_ablate.log)
+    if constexpr (LOSS) {
+      loss_epilogue(acc, it, jt);
+      if (!has_next) break;
+      w = next;
+      continue;
+    }
     f32x4 yrest[EPI == EPI_DTANH ? TJ : 1][EPI == EPI_DTANH ? TI : 1];
     if constexpr (EPI == EPI_DTANH) {
 #pragma unroll
@@ -631,6 +826,24 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
     w = next;
   }
 
+  if constexpr (LOSS) {
+    // the WJ waves' slots in order (deterministic); one partial row per block
+    __syncthreads();
+    for (int f = tid; f < BI; f += C::THREADS) {
+      float t = epi_lds[E_CS + f];
+#pragma unroll
+      for (int m = 1; m < C::WJ; ++m) t += epi_lds[E_CS + m * BI + f];
+      a.part_cs[(int64_t)slot * BI + f] = t;
+    }
+    for (int x = tid; x < KO * BI; x += C::THREADS) {
+      const int o = x / BI, f = x - o * BI;
+      float t = epi_lds[E_DW + o * BI + f];
+#pragma unroll
+      for (int m = 1; m < C::WJ; ++m) t += epi_lds[E_DW + (m * KO + o) * BI + f];
+      a.part_dwo[((int64_t)slot * KO + o) * BI + f] = t;
+    }
+    if (tid < kLossStats) a.part_stats[(int64_t)slot * kLossStats + tid] = epi_lds[E_ST + tid] + epi_lds[E_ST + kLossStats + tid];
+  }
   if constexpr (EPI == EPI_DTANH) {
     // the WJ waves of a feature slice in a fixed order (deterministic); partial[slot / ni][feature]
     __syncthreads();
@@ -1058,6 +1271,57 @@ int vss_linear_tanh_out_bf16x6(void* stream, int64_t rows, int32_t k_in, int32_t
     if (k_out == 2) return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, C, 2>(stream, a, pl);
     return launch<EPI_TANH_OUT, ST_DMA, ST_ROW, C, 6>(stream, a, pl);
   });
+}
+
+int64_t vss_linear_tanh_loss_blocks_bf16x6(int64_t rows, int32_t k_in, int32_t n_out) {
+  using namespace vx6;
+  if (n_out != 256 || !fb_shape_ok<CfgB>(rows, k_in, n_out)) return -1;
+  return fb_plan<CfgB>(rows, k_in, n_out).grid;
+}
+
+int vss_linear_tanh_loss_bf16x6(void* stream, int32_t role, int64_t rows_pad, int64_t rows, int32_t k_in, int32_t n_out,
+                                const float* x, const float* bias, int32_t k_out, const float* w_out, const float* b_out,
+                                const float* action, const float* logprob_old, const float* adv, const double* adv_part,
+                                int32_t adv_nparts, double adv_count, const float* logstd, const float* returns,
+                                const float* values_old, float clip_coef, float clip_lo, float clip_hi, float vf_coef,
+                                int32_t clip_vloss, float* grad_in, float* part_cs, float* part_dwo, float* part_stats,
+                                const uint16_t* w_split) {
+  using namespace vx6;
+  using C = CfgB;
+  const bool actor = role == 0;
+  if ((role != 0 && role != 1) || n_out != 256 || !fb_shape_ok<C>(rows_pad, k_in, n_out) || rows <= 0 || rows > rows_pad ||
+      misaligned(x) || misaligned(grad_in) || misaligned(w_split) || !bias || !w_out || !b_out || !part_cs || !part_dwo ||
+      !part_stats || (actor && (k_out < 1 || k_out > 2 || !action || !logprob_old || !adv || !logstd ||
+                                (adv_part && (adv_nparts < 1 || !(adv_count > 1.0))))) ||
+      (!actor && (k_out != 1 || !returns || (clip_vloss && !values_old))))
+    return VSS_E_ARG;
+  Args a = fb_args(k_in, n_out, w_split, x, grad_in);
+  a.bias = bias;
+  a.w_out = w_out;
+  a.b_out = b_out;
+  a.l_act = action;
+  a.l_logp = logprob_old;
+  a.l_adv = adv;
+  a.adv_part = adv_part;
+  a.adv_nparts = adv_nparts;
+  a.adv_count = adv_count;
+  a.logstd = logstd;
+  a.l_ret = returns;
+  a.l_val = values_old;
+  a.clip = clip_coef;
+  a.clip_lo = clip_lo;
+  a.clip_hi = clip_hi;
+  a.vf_coef = vf_coef;
+  a.inv_n = 1.0f / (float)rows;
+  a.clip_vloss = clip_vloss;
+  a.rows_real = rows;
+  a.part_cs = part_cs;
+  a.part_dwo = part_dwo;
+  a.part_stats = part_stats;
+  const Plan pl = fb_plan<C>(rows_pad, k_in, n_out);
+  if (!actor) return launch<EPI_LOSS_C, ST_DMA, ST_ROW, C, 1>(stream, a, pl);
+  if (k_out == 1) return launch<EPI_LOSS_A, ST_DMA, ST_ROW, C, 1>(stream, a, pl);
+  return launch<EPI_LOSS_A, ST_DMA, ST_ROW, C, 2>(stream, a, pl);
 }
 
 int64_t vss_linear_tanh_backward_chunks_bf16x6(int64_t rows, int32_t k_next, int32_t n_out) {

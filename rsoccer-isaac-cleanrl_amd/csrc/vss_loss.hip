@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 #include "../../include/vss.h"
+#include "vss_loss_row.h"
 
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
 #error "vss_loss.hip targets gfx950 (CDNA4) only"
@@ -108,21 +109,14 @@ __global__ __launch_bounds__(kThreads) void loss_rows_kernel(const RowsArgs p) {
   constexpr int K = kFixed + NA + (DIRECT ? NA + 1 : 0);
   __shared__ float red[kThreads / 64][K];
   const int64_t rows = p.rows, rows_pad = p.rows_pad;
-  // the distribution's per-dimension constants, as torch.distributions.Normal forms them from
-  // scale = exp(logstd): var = scale^2, log_scale = log(scale)
   float var[NA], lsc[NA], bm[NA];
+  vlossrow::actor_consts<NA>(p.logstd, var, lsc);
 #pragma unroll
-  for (int a = 0; a < NA; ++a) {
-    const float s = expf(p.logstd[a]);
-    var[a] = s * s;
-    lsc[a] = logf(s);
-    bm[a] = DIRECT ? p.b_mean[a] : 0.f;
-  }
+  for (int a = 0; a < NA; ++a) bm[a] = DIRECT ? p.b_mean[a] : 0.f;
   const float bv = DIRECT ? p.b_value[0] : 0.f;
   float adv_mean = 0.f, adv_std = 0.f;
   const bool norm = DIRECT && p.adv_part != nullptr;
   if (norm) adv_moments(p.adv_part, p.adv_nparts, p.adv_count, adv_mean, adv_std);
-  const float log_sqrt_2pi = 0.91893853320467274178f;  // math.log(math.sqrt(2 * math.pi)) as fp32
   const float inv_n = p.inv_n, clip = p.clip, lo = p.lo, hi = p.hi;
   float acc[K];
 #pragma unroll
@@ -147,34 +141,19 @@ __global__ __launch_bounds__(kThreads) void loss_rows_kernel(const RowsArgs p) {
       }
       x[a] = p.action[r * NA + a];
     }
-    float nlp = 0.f;
-    float dz[NA];
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-      dz[a] = x[a] - mu[a];
-      nlp += -(dz[a] * dz[a]) / (2.f * var[a]) - lsc[a] - log_sqrt_2pi;
-    }
-    const float logratio = nlp - p.logp_old[r];
-    const float ratio = expf(logratio);
     float A = p.adv[r];
     if (norm) A = (A - adv_mean) / (adv_std + 1e-8f);
-    acc[2] += -logratio;
-    acc[3] += (ratio - 1.f) - logratio;
-    acc[4] += fabsf(ratio - 1.f) > clip ? 1.f : 0.f;
-    const bool in_r = ratio >= lo && ratio <= hi;
-    const float rc = fminf(fmaxf(ratio, lo), hi);
-    const float p1 = -A * ratio, p2 = -A * rc;
-    acc[0] += fmaxf(p1, p2);
-    const float w1 = p1 > p2 ? 1.f : (p1 == p2 ? 0.5f : 0.f);
-    const float w2 = p2 > p1 ? 1.f : (p1 == p2 ? 0.5f : 0.f);
-    const float dratio = w1 * -A + (in_r ? w2 * -A : 0.f);
-    const float dnlp = dratio * ratio;  // x inv_n for the per-row gradient
+    float pg, nlr, kl, cf, gm[NA], lg[NA];
+    vlossrow::actor_row<NA>(mu, x, p.logp_old[r], A, var, lsc, clip, lo, hi, inv_n, pg, nlr, kl, cf, gm, lg);
+    acc[0] += pg;
+    acc[2] += nlr;
+    acc[3] += kl;
+    acc[4] += cf;
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-      const float gm = dnlp * inv_n * (dz[a] / var[a]);
-      p.g_mean[r * NA + a] = gm;
-      acc[kFixed + a] += dnlp * ((dz[a] * dz[a]) / var[a] - 1.f);
-      if constexpr (DIRECT) acc[kFixed + NA + a] += gm;
+      p.g_mean[r * NA + a] = gm[a];
+      acc[kFixed + a] += lg[a];
+      if constexpr (DIRECT) acc[kFixed + NA + a] += gm[a];
     }
     float v;
     if constexpr (DIRECT) {
@@ -184,25 +163,9 @@ __global__ __launch_bounds__(kThreads) void loss_rows_kernel(const RowsArgs p) {
     } else {
       v = p.value[r];
     }
-    const float R = p.ret[r];
-    float dv;
-    if (p.clip_vloss) {
-      const float vo = p.val_old[r];
-      const float d = v - vo;
-      const float vc = vo + fminf(fmaxf(d, -clip), clip);
-      const float eu = v - R, ec = vc - R;
-      const float lu = eu * eu, lc = ec * ec;
-      acc[1] += fmaxf(lu, lc);
-      const float wu = lu > lc ? 1.f : (lu == lc ? 0.5f : 0.f);
-      const float wc = lc > lu ? 1.f : (lu == lc ? 0.5f : 0.f);
-      const bool in_v = d >= -clip && d <= clip;
-      dv = 0.5f * (wu * 2.f * eu + (in_v ? wc * 2.f * ec : 0.f));
-    } else {
-      const float e = v - R;
-      acc[1] += e * e;
-      dv = e;  // 0.5 x 2 (v - R)
-    }
-    const float gv = p.vf_coef * dv * inv_n;
+    float vl, gv;
+    vlossrow::critic_row(v, p.ret[r], p.clip_vloss ? p.val_old[r] : 0.f, p.clip_vloss, clip, p.vf_coef, inv_n, vl, gv);
+    acc[1] += vl;
     p.g_value[r] = gv;
     if constexpr (DIRECT) acc[kFixed + 2 * NA] += gv;
   }
@@ -263,6 +226,53 @@ __global__ __launch_bounds__(kThreads) void loss_finish_kernel(int blocks, const
       for (int a = 0; a < NA; ++a) db_mean[a] = tot[kFixed + NA + a];
       db_value[0] = tot[kFixed + 2 * NA];
     }
+  }
+}
+
+// the fused loss epilogue's per-block sums (vss_gemm_x6.hip EPI_LOSS_A / EPI_LOSS_C, vlossrow::kBlockStats
+// layout) -> the loss, its statistics, the log-std gradient and the output biases' gradients, as
+// loss_finish_kernel<NA, true> forms them
+template <int NA>
+__global__ __launch_bounds__(kThreads) void fused_finish_kernel(int actor_blocks, const float* __restrict__ actor,
+                                                                int critic_blocks, const float* __restrict__ critic,
+                                                                const float* __restrict__ logstd, float ent_coef,
+                                                                float vf_coef, float n, float inv_n,
+                                                                float* __restrict__ g_logstd, float* __restrict__ loss_out,
+                                                                float* __restrict__ stats, float* __restrict__ db_mean,
+                                                                float* __restrict__ db_value) {
+  constexpr int S = vlossrow::kBlockStats;
+  __shared__ float tot[2 * S];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int k = wv; k < 2 * S; k += kThreads / 64) {
+    const bool c = k >= S;
+    const float* p = c ? critic : actor;
+    const int blocks = c ? critic_blocks : actor_blocks, kk = c ? k - S : k;
+    float s = 0.f;
+    for (int b = lane; b < blocks; b += 64) s += p[(int64_t)b * S + kk];
+    s = wave_sum(s);
+    if (lane == 0) tot[k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float* ta = tot;
+    const float* tc = tot + S;
+    float ent = 0.f;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) ent += 1.41893853320467274178f + logf(expf(logstd[a]));
+    const float pg = ta[0] / n, vl = 0.5f * (tc[1] / n);
+    loss_out[0] = pg - ent_coef * ent + vl * vf_coef;
+    stats[0] = pg;
+    stats[1] = vl;
+    stats[2] = ent;
+    stats[3] = ta[2] / n;
+    stats[4] = ta[3] / n;
+    stats[5] = ta[4] / n;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      g_logstd[a] = ta[kFixed + a] * inv_n - ent_coef;
+      db_mean[a] = ta[kFixed + NA + a];
+    }
+    db_value[0] = tc[kFixed];
   }
 }
 
@@ -467,6 +477,28 @@ int vss_ppo_loss_direct(void* stream, int64_t rows, int64_t rows_pad, int32_t n_
                           partial};
   return vloss::dispatch<true>(stream, n_act, a, ent_coef, grad_logstd, loss_out, stats_out, grad_mean_bias,
                                grad_value_bias);
+}
+
+int vss_ppo_loss_fused_finish(void* stream, int64_t rows, int32_t n_act, int64_t actor_blocks, const float* actor_stats,
+                              int64_t critic_blocks, const float* critic_stats, const float* logstd, float ent_coef,
+                              float vf_coef, float* grad_logstd, float* grad_mean_bias, float* grad_value_bias,
+                              float* loss_out, float* stats_out) {
+  if (rows <= 0 || actor_blocks < 1 || critic_blocks < 1 || !actor_stats || !critic_stats || !logstd || !grad_logstd ||
+      !grad_mean_bias || !grad_value_bias || !loss_out || !stats_out)
+    return VSS_E_ARG;
+  const dim3 grid(1), block(vloss::kThreads);
+  const float n = (float)rows, inv_n = 1.0f / (float)rows;
+  if (n_act == 1)
+    hipLaunchKernelGGL((vloss::fused_finish_kernel<1>), grid, block, 0, (hipStream_t)stream, (int)actor_blocks,
+                       actor_stats, (int)critic_blocks, critic_stats, logstd, ent_coef, vf_coef, n, inv_n, grad_logstd,
+                       loss_out, stats_out, grad_mean_bias, grad_value_bias);
+  else if (n_act == 2)
+    hipLaunchKernelGGL((vloss::fused_finish_kernel<2>), grid, block, 0, (hipStream_t)stream, (int)actor_blocks,
+                       actor_stats, (int)critic_blocks, critic_stats, logstd, ent_coef, vf_coef, n, inv_n, grad_logstd,
+                       loss_out, stats_out, grad_mean_bias, grad_value_bias);
+  else
+    return VSS_E_ARG;
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 
 int64_t vss_minibatch_gather_parts(int64_t mb) { return mb <= 0 ? -1 : vloss::gather_scalar_blocks(mb); }

@@ -55,9 +55,11 @@ from torch.distributions.normal import Normal
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from envs._gym import Box, ObservationWrapper  # noqa: E402
-from vss_amd.loss import N_ACT, adv_part_sum, minibatch_gather, minibatch_gather_parts, ppo_loss, ppo_loss_direct  # noqa: E402
+from vss_amd.loss import (N_ACT, adv_part_sum, minibatch_gather, minibatch_gather_parts, ppo_loss,  # noqa: E402
+                          ppo_loss_direct, ppo_loss_fused_finish)
 from vss_amd.update import (first_wgrad_ok, gemm_shape_ok, linear_tanh, linear_tanh_backward, linear_tanh_backward_mixed,  # noqa: E402
-                            linear_tanh_mixed, linear_tanh_out, linear_tanh_out_mixed, linear_tanh_out_ok,
+                            linear_tanh_loss_x6, linear_tanh_loss_x6_ok, linear_tanh_mixed, linear_tanh_out,
+                            linear_tanh_out_mixed, linear_tanh_out_ok,
                             linear_tanh_out_x6, output_backward, output_backward_direct, output_backward_direct_ok,
                             output_backward_ok, sum_parts, weight_grad_mixed, weight_planes, x6_ok)
 
@@ -331,6 +333,9 @@ def _nets_planes(nets, rows: int):
 # (The round-4 A/B switches VSS_UPDATE_MLP=split, VSS_OUTPUT_FWD/BWD=0 and VSS_WEIGHT_PLANES=0, each
 # strictly slower, are retired from the product: tools/ab_switches_r04.patch re-adds them for A/B runs.)
 UPDATE_GEMM = os.environ.get("VSS_UPDATE_GEMM", "x6")
+# direct_minibatch's loss folded into the last hidden layer's x6 launch (vss_linear_tanh_loss_bf16x6) where
+# the output layers allow it; "0" keeps the separate output-layer / loss / output-backward launches
+FUSED_LOSS = os.environ.get("VSS_FUSED_LOSS", "1") != "0"
 
 
 def _fused_mlp_ok(seq: nn.Sequential) -> bool:
@@ -729,6 +734,17 @@ def direct_minibatch_ok(agent, args, flat) -> bool:
                for p in agent.parameters() if p.requires_grad)
 
 
+def _fused_loss_ok(agent, rows_pad: int) -> bool:
+    """Whether direct_minibatch folds the loss into the last hidden layers' launches: the actor's 1 or 2
+    outputs, the critic's value (direct_minibatch_ok's networks otherwise)."""
+    for seq in (agent.actor_mean, agent.critic):
+        ws, _ = _mlp_wb(seq)
+        (n, k), k_out = ws[-2].shape, ws[-1].shape[0]
+        if not linear_tanh_loss_x6_ok(rows_pad, k, n, k_out):
+            return False
+    return _mlp_wb(agent.critic)[0][-1].shape[0] == 1
+
+
 def direct_minibatch(agent, args, obs, act, logp, adv, adv_part, adv_count, ret, val):
     """One update minibatch (ppo…:331-352: the networks, the clipped losses, loss.backward() into the
     zeroed gradients) as a fixed launch sequence writing every gradient into its FlatGrads view.  obs / act
@@ -754,8 +770,37 @@ def direct_minibatch(agent, args, obs, act, logp, adv, adv_part, adv_count, ret,
         gz, gb, _ = output_backward_direct(g, ws[-1], hs[-1], out_db=d[2 * n - 3], out_dw=d[2 * n - 2], defer=defer)
         _backward_layers(hs, ws, pb, gz, gb, n - 2, d, [None] * (2 * n), defer)
 
+    def fused(seq, is_actor, defer):
+        # the hidden layers below the last, then the last hidden layer + output layer + this network's loss
+        # terms + the output layer's backward in one launch
+        ws, bs = _mlp_wb(seq)
+        pf, pb = planes[id(seq)]
+        n = len(ws)
+        d = [t.grad for w, b in zip(ws, bs) for t in (w, b)]
+        hs = [obs]
+        for layer in range(n - 2):
+            hs.append(linear_tanh_mixed(hs[-1], ws[layer], bs[layer], planes=pf.get(layer)))
+        role = dict(act=act, logp=logp, adv=adv, adv_part=adv_part, adv_count=adv_count,
+                    logstd=agent.actor_logstd) if is_actor else dict(ret=ret, val=val)
+        gz, gb, _, st = linear_tanh_loss_x6(hs[-1], ws[-2], bs[-2], ws[-1], bs[-1], logp.shape[0], is_actor,
+                                            planes=pf.get(n - 2), clip_coef=args.clip_coef, vf_coef=args.vf_coef,
+                                            clip_vloss=args.clip_vloss, out_db=d[2 * n - 3], out_dw=d[2 * n - 2],
+                                            defer=defer, **role)
+        return (hs, ws, pb, gz, gb, n, d), st
+
     # one stream: the critic's launches on a second stream beside the actor's were measured and not kept
     # (4,095 envs: 0.153 vs 0.154 s per update; 65,536: 2.33 vs 2.30 s -- concurrent GEMMs contend)
+    if FUSED_LOSS and _fused_loss_ok(agent, obs.shape[0]):
+        with torch.no_grad():
+            defer = []
+            a_net, a_st = fused(agent.actor_mean, True, defer)
+            c_net, c_st = fused(agent.critic, False, defer)
+            loss, stats = ppo_loss_fused_finish(a_st, c_st, logp.shape[0], agent.actor_logstd, args.ent_coef,
+                                                args.vf_coef, agent.actor_logstd.grad, a_net[6][-1], c_net[6][-1])
+            for hs, ws, pb, gz, gb, n, d in (a_net, c_net):
+                _backward_layers(hs, ws, pb, gz, gb, n - 2, d, [None] * (2 * n), defer)
+            sum_parts(defer)
+        return loss, tuple(stats[i] for i in range(6))
     with torch.no_grad():
         actor, critic = forward(agent.actor_mean), forward(agent.critic)
         (_, _, ba, pa, _, da), (_, _, bc, pc, _, dc) = actor, critic

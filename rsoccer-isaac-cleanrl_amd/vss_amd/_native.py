@@ -23,7 +23,8 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "vss.h"
 # the sources the Makefile stamps into the library, in its order (csrc/Makefile STAMPED)
 STAMPED = (os.path.join(CSRC, "vss_step.hip"), os.path.join(CSRC, "vss_update.hip"),
            os.path.join(CSRC, "vss_policy.hip"), os.path.join(CSRC, "vss_gemm_x6.hip"),
-           os.path.join(CSRC, "vss_loss.hip"), os.path.join(CSRC, "vss_optim.hip"), HEADER,
+           os.path.join(CSRC, "vss_loss.hip"), os.path.join(CSRC, "vss_optim.hip"),
+           os.path.join(CSRC, "vss_loss_row.h"), HEADER,
            os.path.join(CSRC, "Makefile"))
 
 ABI_VERSION = 2
@@ -43,7 +44,8 @@ EXPORTED = ("vss_abi_version", "vss_source_hash", "vss_error_string", "vss_step"
             "vss_grad_sq_partials_count", "vss_grad_sq_partials", "vss_adam_step_clipped", "vss_sum_parts",
             "vss_output_backward_direct_chunks", "vss_output_backward_direct", "vss_ppo_loss_direct_scratch_floats",
             "vss_ppo_loss_direct", "vss_minibatch_gather_parts", "vss_minibatch_gather", "vss_adv_part_sum",
-            "vss_first_layer_bf16x6")
+            "vss_first_layer_bf16x6", "vss_linear_tanh_loss_blocks_bf16x6", "vss_linear_tanh_loss_bf16x6",
+            "vss_ppo_loss_fused_finish")
 
 
 class VssParams(ctypes.Structure):
@@ -214,6 +216,13 @@ def load() -> ctypes.CDLL:
     L.vss_adv_part_sum.restype = ctypes.c_int
     L.vss_first_layer_bf16x6.argtypes = [P, i64, i32, i32, P, P, P, P]
     L.vss_first_layer_bf16x6.restype = ctypes.c_int
+    L.vss_linear_tanh_loss_blocks_bf16x6.argtypes = [i64, i32, i32]
+    L.vss_linear_tanh_loss_blocks_bf16x6.restype = i64
+    L.vss_linear_tanh_loss_bf16x6.argtypes = ([P, i32, i64, i64, i32, i32, P, P, i32, P, P] + [P] * 4
+                                              + [i32, ctypes.c_double] + [P] * 3 + [f32] * 4 + [i32] + [P] * 5)
+    L.vss_linear_tanh_loss_bf16x6.restype = ctypes.c_int
+    L.vss_ppo_loss_fused_finish.argtypes = [P, i64, i32, i64, P, i64, P, P, f32, f32] + [P] * 5
+    L.vss_ppo_loss_fused_finish.restype = ctypes.c_int
     if L.vss_abi_version() != ABI_VERSION:
         raise NativeError(f"libvss_amd ABI {L.vss_abi_version()} != expected {ABI_VERSION}")
     _lib = L

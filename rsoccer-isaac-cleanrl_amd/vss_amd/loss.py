@@ -162,6 +162,30 @@ def ppo_loss_direct(mean_parts, mean_bias, value_parts, value_bias, logstd, acti
     return g_mean, g_value, loss, stats
 
 
+def ppo_loss_fused_finish(actor_stats, critic_stats, rows: int, logstd, ent_coef, vf_coef, grad_logstd,
+                          grad_mean_bias, grad_value_bias):
+    """vss_ppo_loss_fused_finish: the per-block loss sums of the actor's and the critic's fused loss
+    launches (update.linear_tanh_loss_x6) -> (loss, stats (6,)); writes d loss / d logstd and the output
+    layers' bias gradients into grad_logstd, grad_mean_bias, grad_value_bias as ppo_loss_direct."""
+    n_act = logstd.numel()
+    for t in (actor_stats, critic_stats, logstd, grad_logstd, grad_mean_bias, grad_value_bias):
+        if t.dtype != torch.float32 or t.device != actor_stats.device or not t.is_contiguous():
+            raise ValueError("ppo_loss_fused_finish: contiguous fp32 tensors on one device")
+    if n_act not in (1, 2) or actor_stats.dim() != 2 or actor_stats.shape[1] != 32 or critic_stats.dim() != 2 \
+            or critic_stats.shape[1] != 32 or grad_logstd.numel() != n_act or grad_mean_bias.numel() != n_act \
+            or grad_value_bias.numel() != 1 or rows <= 0:
+        raise ValueError(f"ppo_loss_fused_finish: stats {tuple(actor_stats.shape)} / {tuple(critic_stats.shape)}, "
+                         f"{n_act} actions")
+    f32 = dict(device=actor_stats.device, dtype=torch.float32)
+    loss, stats = torch.empty((), **f32), torch.empty(6, **f32)
+    N.check(N.load().vss_ppo_loss_fused_finish(
+        N.stream_of(actor_stats.device), rows, n_act, actor_stats.shape[0], actor_stats.data_ptr(), critic_stats.shape[0],
+        critic_stats.data_ptr(), logstd.data_ptr(), float(ent_coef), float(vf_coef), grad_logstd.data_ptr(),
+        grad_mean_bias.data_ptr(), grad_value_bias.data_ptr(), loss.data_ptr(), stats.data_ptr()),
+        "vss_ppo_loss_fused_finish")
+    return loss, stats
+
+
 def minibatch_gather_parts(mb: int) -> int:
     """Rows of the (sum, sum of squares) parts minibatch_gather writes for mb minibatch rows."""
     return int(N.load().vss_minibatch_gather_parts(mb))

@@ -264,6 +264,63 @@ def output_backward_direct(g_out: torch.Tensor, w_out: torch.Tensor, y: torch.Te
     return gz, _reduce_parts(bpart, out_db, defer), _reduce_parts(wpart, out_dw, defer)
 
 
+def linear_tanh_loss_x6_ok(rows_pad: int, k: int, n: int, k_out: int) -> bool:
+    """Shapes vss_linear_tanh_loss_bf16x6 takes: a 256-wide last hidden layer on the x6 shapes, 1 or 2
+    outputs."""
+    return n == 256 and k_out in (1, 2) and x6_ok(rows_pad, k, n)
+
+
+def linear_tanh_loss_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out: torch.Tensor, b_out: torch.Tensor,
+                        rows: int, actor: bool, *, planes: torch.Tensor | None = None, act=None, logp=None, adv=None,
+                        adv_part=None, adv_count: float = 0.0, logstd=None, ret=None, val=None, clip_coef: float = 0.2,
+                        vf_coef: float = 0.5, clip_vloss: bool = False, out_db=None, out_dw=None, defer=None):
+    """The last hidden layer, the output layer, one network's loss terms and the output layer's backward
+    in ONE x6 launch (vss_linear_tanh_loss_bf16x6, direct_minibatch): x (rows_pad, k) the layer's input,
+    w (256, k) / b its weight and bias (planes: weight_planes() of w, or None to split it here), w_out /
+    b_out the output layer's; actor: act / logp / adv (RAW, normalised from adv_part over adv_count as
+    ppo_loss_direct) / logstd, else ret / val.  Returns (gz (rows_pad, 256) the hidden layer's
+    pre-activation gradient, its bias gradient, the output weight's gradient (both into out_db / out_dw,
+    summed through `defer` when given), the per-block loss sums for ppo_loss_fused_finish)."""
+    rows_pad, k = x.shape
+    n, k_out = w.shape[0], w_out.shape[0]
+    _x6_check("vss_linear_tanh_loss_bf16x6", w.shape == (n, k) and b.shape == (n,) and w_out.shape == (k_out, n)
+              and b_out.shape == (k_out,) and 0 < rows <= rows_pad and linear_tanh_loss_x6_ok(rows_pad, k, n, k_out)
+              and (not actor or k_out == 2 or k_out == 1) and (actor or k_out == 1), x, w, b, w_out)
+    rows_t = (act, logp, adv, logstd) if actor else (ret,) + ((val,) if clip_vloss else ())
+    for t in rows_t:
+        if t is None or t.dtype != torch.float32 or t.device != x.device or not t.is_contiguous():
+            raise ValueError("linear_tanh_loss_x6: the role's loss inputs as contiguous fp32 tensors on the device")
+    if actor and (act.shape[0] < rows_pad or act.shape[1] != k_out or logp.shape[0] < rows or adv.shape[0] < rows
+                  or logstd.numel() != k_out):
+        raise ValueError(f"linear_tanh_loss_x6: actor inputs for {rows} rows and {k_out} actions")
+    if not actor and (ret.shape[0] < rows or (clip_vloss and val.shape[0] < rows)):
+        raise ValueError(f"linear_tanh_loss_x6: critic inputs for {rows} rows")
+    if adv_part is not None and (adv_part.dtype != torch.float64 or adv_part.device != x.device
+                                 or adv_part.dim() != 2 or adv_part.shape[1] != 2 or not adv_part.is_contiguous()):
+        raise ValueError("linear_tanh_loss_x6: adv_part must be a contiguous (parts, 2) fp64 tensor on the device")
+    lib = N.load()
+    x, b, w_out, b_out = x.contiguous(), b.contiguous(), w_out.contiguous(), b_out.contiguous()
+    if planes is None:  # the fused entry takes only the planes
+        planes = weight_planes([(w.contiguous(), False)])[0]
+    _, pp, keep = _w_and_planes(w, planes)
+    blocks = lib.vss_linear_tanh_loss_blocks_bf16x6(rows_pad, k, n)
+    f32 = dict(device=x.device, dtype=torch.float32)
+    gz = torch.empty((rows_pad, n), **f32)
+    part_cs = torch.empty((blocks, n), **f32)
+    part_dw = torch.empty((blocks, k_out, n), **f32)
+    stats = torch.empty((blocks, 32), **f32)
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    c = float(clip_coef)
+    N.check(lib.vss_linear_tanh_loss_bf16x6(
+        N.stream_of(x.device), 0 if actor else 1, rows_pad, rows, k, n, x.data_ptr(), b.data_ptr(), k_out,
+        w_out.data_ptr(), b_out.data_ptr(), ptr(act), ptr(logp), ptr(adv), ptr(adv_part),
+        adv_part.shape[0] if adv_part is not None else 0, float(adv_count), ptr(logstd), ptr(ret),
+        ptr(val) if clip_vloss else None, c, 1 - c, 1 + c, float(vf_coef), int(bool(clip_vloss)), gz.data_ptr(),
+        part_cs.data_ptr(), part_dw.data_ptr(), stats.data_ptr(), pp), "vss_linear_tanh_loss_bf16x6")
+    del keep
+    return gz, _reduce_parts(part_cs, out_db, defer), _reduce_parts(part_dw, out_dw, defer), stats
+
+
 # ---- the same GEMMs in fp32 arithmetic on the bf16 matrix cores (csrc/vss_gemm_x6.hip) ----------------
 # Every operand is split exactly into three bf16 parts and each product is summed from the six partial
 # products above 2^-23 |a||b| in fp32 (tests/test_gemm_x6.py: the error is that of an fp32 GEMM).

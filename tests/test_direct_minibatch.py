@@ -11,8 +11,10 @@ import torch
 
 import ppo_continuous_action_isaacgym as P
 from test_ppo import _args, _synthetic_batch, make_agent
-from vss_amd.loss import N_ACT, adv_part_sum, minibatch_gather, minibatch_gather_parts, ppo_loss, ppo_loss_direct
-from vss_amd.update import output_backward, output_backward_direct, output_backward_direct_ok
+from vss_amd.loss import (N_ACT, adv_part_sum, minibatch_gather, minibatch_gather_parts, ppo_loss, ppo_loss_direct,
+                          ppo_loss_fused_finish)
+from vss_amd.update import (linear_tanh_loss_x6, linear_tanh_loss_x6_ok, linear_tanh_out_x6, output_backward,
+                            output_backward_direct, output_backward_direct_ok)
 
 
 def test_direct_shapes_cpu():
@@ -21,6 +23,14 @@ def test_direct_shapes_cpu():
     assert not output_backward_direct_ok(5, 256) and not output_backward_direct_ok(2, 384)
     assert minibatch_gather_parts(1) == 1 and minibatch_gather_parts(131040) == 256
     assert N_ACT == (1, 2, 3, 4, 6, 8)
+
+
+def test_fused_loss_shapes_cpu():
+    """The fused loss launch's shapes: a 256-wide last hidden layer on the x6 rows, 1 or 2 outputs
+    (6 actions keep the separate launches)."""
+    assert linear_tanh_loss_x6_ok(131072, 256, 256, 2) and linear_tanh_loss_x6_ok(256, 256, 256, 1)
+    assert not linear_tanh_loss_x6_ok(131072, 256, 256, 6) and not linear_tanh_loss_x6_ok(131040, 256, 256, 2)
+    assert not linear_tanh_loss_x6_ok(4096, 256, 512, 2)
 
 
 def test_direct_minibatch_not_for_cpu_or_amp():
@@ -126,19 +136,69 @@ def test_ppo_loss_direct_matches_loss_on_summed_outputs_gpu(norm, clip_vloss):
     assert float((dbv.double() - gv.double().sum()).abs().max()) <= 1e-6 * float(gv.double().abs().sum())
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,rows_pad,n_act,norm,clip_vloss", [
+    (131040, 131072, 2, True, False), (65536, 65536, 2, True, True), (1000, 1024, 1, False, True)])
+def test_fused_loss_matches_separate_launches_gpu(rows, rows_pad, n_act, norm, clip_vloss):
+    """vss_linear_tanh_loss_bf16x6 (actor and critic) + vss_ppo_loss_fused_finish = the separate launches
+    direct_minibatch otherwise runs (vss_linear_tanh_out_bf16x6 with parts, vss_ppo_loss_direct,
+    vss_output_backward_direct): the hidden layer's gradient, its bias and the output weight's gradients,
+    the loss, its statistics and the log-std / output-bias gradients within fp32 summation-order rounding;
+    the padding rows' gradient exactly zero."""
+    g = torch.Generator(device="cuda").manual_seed(7)
+    rn = lambda *s: torch.randn(*s, device="cuda", generator=g)  # noqa: E731
+    xa, xc = torch.tanh(rn(rows_pad, 256)), torch.tanh(rn(rows_pad, 256))
+    wa, wc = rn(256, 256) / 16, rn(256, 256) / 16
+    ba, bc = rn(256) * 0.1, rn(256) * 0.1
+    woa, woc = rn(n_act, 256) / 16, rn(1, 256) / 16
+    boa, boc = rn(n_act) * 0.1, rn(1)
+    logstd = rn(1, n_act) * 0.1
+    act = rn(rows_pad, n_act) * 0.3
+    logp, adv, ret, val = rn(rows) - 1.0, rn(rows), rn(rows), rn(rows)
+    part = None
+    if norm:
+        a = adv.double()
+        part = torch.stack([a.sum(), (a * a).sum()]).view(1, 2).contiguous()
+    kw = dict(clip_coef=0.2, vf_coef=0.5, clip_vloss=clip_vloss)
+    # the separate launches
+    ya, pa = linear_tanh_out_x6(xa, wa, ba, woa, boa, parts=True)
+    yc, pc = linear_tanh_out_x6(xc, wc, bc, woc, boc, parts=True)
+    gl0, dbm0, dbv0 = torch.empty_like(logstd), torch.empty(n_act, device="cuda"), torch.empty(1, device="cuda")
+    gm, gv, loss0, st0 = ppo_loss_direct(pa, boa, pc, boc, logstd, act, logp, adv, part, rows, ret, val, 0.2, 0.01, 0.5,
+                                         clip_vloss, gl0, dbm0, dbv0)
+    ref = [output_backward_direct(gm, woa, ya), output_backward_direct(gv, woc, yc)]
+    # the fused launches
+    gl1, dbm1, dbv1 = torch.empty_like(logstd), torch.empty(n_act, device="cuda"), torch.empty(1, device="cuda")
+    fa = linear_tanh_loss_x6(xa, wa, ba, woa, boa, rows, True, act=act, logp=logp, adv=adv, adv_part=part,
+                             adv_count=rows, logstd=logstd, **kw)
+    fc = linear_tanh_loss_x6(xc, wc, bc, woc, boc, rows, False, ret=ret, val=val, **kw)
+    loss1, st1 = ppo_loss_fused_finish(fa[3], fc[3], rows, logstd, 0.01, 0.5, gl1, dbm1, dbv1)
+    for (gz0, db0, dw0), (gz1, db1, dw1, _) in zip(ref, (fa, fc)):
+        assert torch.equal(gz1[rows:], torch.zeros_like(gz1[rows:]))
+        for got, want in ((gz1, gz0), (db1, db0), (dw1, dw0)):
+            assert float((got - want).abs().max()) <= 2e-5 * float(want.abs().max()), (got.shape, want.shape)
+    torch.testing.assert_close(loss1, loss0, rtol=2e-5, atol=1e-6)
+    torch.testing.assert_close(st1, st0, rtol=2e-5, atol=1e-6)
+    torch.testing.assert_close(gl1, gl0, rtol=2e-5, atol=1e-6)
+    for got, want in ((dbm1, dbm0), (dbv1, dbv0)):
+        assert float((got - want).abs().max()) <= 2e-5 * max(float(want.abs().max()), 1e-3)
+
+
 def _grads(agent):
     return [p.grad.detach().clone() for p in agent.parameters()]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,nmb,act_dim,norm_adv,clip_vloss", [
-    (262080, 2, 2, True, False),   # 131,040-row minibatches (4,095 envs): 32 padding rows
-    (32768, 2, 2, True, True), (32768, 4, 6, False, True), (4096, 2, 2, True, False)])
-def test_direct_minibatch_matches_autograd_path_gpu(n, nmb, act_dim, norm_adv, clip_vloss):
+@pytest.mark.parametrize("n,nmb,act_dim,norm_adv,clip_vloss,fused", [
+    (262080, 2, 2, True, False, True),   # 131,040-row minibatches (4,095 envs): 32 padding rows
+    (262080, 2, 2, True, False, False), (32768, 2, 2, True, True, True), (32768, 2, 1, False, True, True),
+    (32768, 4, 6, False, True, True), (4096, 2, 2, True, False, True)])
+def test_direct_minibatch_matches_autograd_path_gpu(n, nmb, act_dim, norm_adv, clip_vloss, fused, monkeypatch):
     """One minibatch through direct_minibatch (gather, forward, loss, backward into the FlatGrads views)
     against the autograd path on the same rows (index_select + normalize_advantages + minibatch_losses +
     zeroed_backward): every parameter's gradient within 2e-5 of its largest entry, the statistics within
     fp32 rounding; every gradient view written (the flat buffer starts as NaN)."""
+    monkeypatch.setattr(P, "FUSED_LOSS", fused)  # the loss in the last hidden layers' launches, or apart
     args = _args(norm_adv=norm_adv, clip_vloss=clip_vloss, num_minibatches=nmb)
     g = torch.Generator().manual_seed(11)
     obs, _, logp, adv, ret, val = [t.cuda() for t in _synthetic_batch(5, n)]

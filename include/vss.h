@@ -482,6 +482,13 @@ int vss_ppo_loss_fused_finish(void* stream, int64_t rows, int32_t n_act, int64_t
                               int64_t critic_blocks, const float* critic_stats, const float* logstd, float ent_coef,
                               float vf_coef, float* grad_logstd, float* grad_mean_bias, float* grad_value_bias,
                               float* loss_out, float* stats_out);
+/* vss_randperm: the epoch's minibatch permutation (ppo…:309, torch.randperm(batch)): out (n,) int64 a
+ * uniformly random permutation of [0, n) determined by seed[0] (one int64 on the device, drawn from the
+ * update's generator), 0 < n < 2^31.  scratch: vss_randperm_scratch_bytes(n) bytes (-1 for a bad n),
+ * 256-B aligned.  Each index gets 32 random bits (splitmix64 of seed and index); a stable radix sort on
+ * them (4 passes, hipcub) orders the indices; ties keep index order. */
+int64_t vss_randperm_scratch_bytes(int64_t n);
+int vss_randperm(void* stream, int64_t n, const int64_t* seed, int64_t* out, void* scratch, int64_t scratch_bytes);
 int64_t vss_minibatch_gather_parts(int64_t mb);
 int vss_minibatch_gather(void* stream, int64_t mb, int64_t rows_pad, int64_t batch, const int64_t* inds, int64_t obs_w,
                          int64_t act_w, const float* b_obs, const float* b_act, const float* b_logp, const float* b_adv,

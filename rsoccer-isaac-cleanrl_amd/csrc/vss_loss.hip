@@ -24,6 +24,7 @@
 
 #include "../../include/vss.h"
 #include "vss_loss_row.h"
+#include <hipcub/hipcub.hpp>
 
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
 #error "vss_loss.hip targets gfx950 (CDNA4) only"
@@ -430,6 +431,46 @@ static int64_t gather_scalar_blocks(int64_t mb) {
   return b < 1 ? 1 : (b > kGatherScalarBlocks ? kGatherScalarBlocks : b);
 }
 
+
+// ---- the epoch's minibatch permutation (ppo…:309, torch.randperm(batch)): a uniformly random
+// permutation from one 64-bit seed drawn from the update's generator.  Each index i gets the key
+// (32 random bits << 32) | i, with the random bits from splitmix64 of (seed, i); a stable radix sort on
+// the high 32 bits (4 passes) orders the indices by their random bits (ties, ~n^2 / 2^33 pairs, keep index
+// order), and the low 32 bits of the sorted keys are the permutation, written in place as int64.  Against
+// torch's randperm (64-bit keys: 8 passes, plus its duplicate-key pass) half the sort traffic.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kThreads) void perm_keys_kernel(int64_t n, const int64_t* __restrict__ seed,
+                                                             uint64_t* __restrict__ keys) {
+  const uint64_t s = (uint64_t)seed[0];
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    const uint64_t r = splitmix64(s + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull);
+    keys[i] = (r & 0xFFFFFFFF00000000ull) | (uint64_t)i;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void perm_index_kernel(int64_t n, uint64_t* __restrict__ keys) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) keys[i] &= 0xFFFFFFFFull;
+}
+
+static size_t perm_sort_bytes(int64_t n) {
+  size_t bytes = 0;
+  if (hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)n, 32, 64,
+                                        (hipStream_t)0) != hipSuccess)
+    return 0;
+  return bytes;
+}
+
+static int64_t perm_grid(int64_t n) {
+  const int64_t g = (n + kThreads - 1) / kThreads;
+  return g < 1 ? 1 : (g > 4096 ? 4096 : g);
+}
 }  // namespace vloss
 
 extern "C" {
@@ -498,6 +539,32 @@ int vss_ppo_loss_fused_finish(void* stream, int64_t rows, int32_t n_act, int64_t
                        loss_out, stats_out, grad_mean_bias, grad_value_bias);
   else
     return VSS_E_ARG;
+  return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+}
+
+int64_t vss_randperm_scratch_bytes(int64_t n) {
+  if (n <= 0 || n > 0xFFFFFFFFll || n > 0x7FFFFFFFll) return -1;
+  const size_t sort = vloss::perm_sort_bytes(n);
+  if (sort == 0) return -1;
+  return ((n * 8 + 255) / 256) * 256 + (int64_t)sort;
+}
+
+int vss_randperm(void* stream, int64_t n, const int64_t* seed, int64_t* out, void* scratch, int64_t scratch_bytes) {
+  const int64_t need = vss_randperm_scratch_bytes(n);
+  if (need < 0 || !seed || !out || !scratch || scratch_bytes < need || (reinterpret_cast<uintptr_t>(scratch) & 255) ||
+      (reinterpret_cast<uintptr_t>(out) & 7))
+    return VSS_E_ARG;
+  uint64_t* keys = static_cast<uint64_t*>(scratch);
+  char* temp = static_cast<char*>(scratch) + ((n * 8 + 255) / 256) * 256;
+  size_t temp_bytes = (size_t)(scratch_bytes - ((n * 8 + 255) / 256) * 256);
+  const hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)vloss::perm_grid(n)), block(vloss::kThreads);
+  hipLaunchKernelGGL(vloss::perm_keys_kernel, grid, block, 0, st, n, seed, keys);
+  if (hipGetLastError() != hipSuccess) return VSS_E_LAUNCH;
+  if (hipcub::DeviceRadixSort::SortKeys(temp, temp_bytes, keys, reinterpret_cast<uint64_t*>(out), (int)n, 32, 64, st) !=
+      hipSuccess)
+    return VSS_E_LAUNCH;
+  hipLaunchKernelGGL(vloss::perm_index_kernel, grid, block, 0, st, n, reinterpret_cast<uint64_t*>(out));
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
 }
 

@@ -56,7 +56,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from envs._gym import Box, ObservationWrapper  # noqa: E402
 from vss_amd.loss import (N_ACT, adv_part_sum, minibatch_gather, minibatch_gather_parts, ppo_loss,  # noqa: E402
-                          ppo_loss_direct, ppo_loss_fused_finish)
+                          ppo_loss_direct, ppo_loss_fused_finish, randperm)
 from vss_amd.update import (first_wgrad_ok, gemm_shape_ok, linear_tanh, linear_tanh_backward, linear_tanh_backward_mixed,  # noqa: E402
                             linear_tanh_loss_x6, linear_tanh_loss_x6_ok, linear_tanh_mixed, linear_tanh_out,
                             linear_tanh_out_mixed, linear_tanh_out_ok,
@@ -336,6 +336,9 @@ UPDATE_GEMM = os.environ.get("VSS_UPDATE_GEMM", "x6")
 # direct_minibatch's loss folded into the last hidden layer's x6 launch (vss_linear_tanh_loss_bf16x6) where
 # the output layers allow it; "0" keeps the separate output-layer / loss / output-backward launches
 FUSED_LOSS = os.environ.get("VSS_FUSED_LOSS", "1") != "0"
+# the epochs' permutations on a ROCm device from vss_randperm (one seed per epoch from the update's
+# generator); VSS_RANDPERM=torch keeps torch.randperm
+RANDPERM_HIP = os.environ.get("VSS_RANDPERM", "hip") != "torch"
 
 
 def _fused_mlp_ok(seq: nn.Sequential) -> bool:
@@ -991,9 +994,9 @@ _SIDE_STREAMS = {}
 
 class EpochPermutations:
     """The update's per-epoch minibatch permutations (ppo…:309, torch.randperm(batch) from `gen`, in epoch
-    order).  On a ROCm device with ahead=True (no --target-kl early stop, so every epoch's permutation is
-    drawn), epoch e + 1's is drawn on a side stream while epoch e's minibatches run: torch's randperm is
-    ~25 sort launches (~0.25 ms at 4,095 envs), which then overlap the GEMMs instead of preceding the
+    order; on a ROCm device vss_randperm from one seed per epoch drawn from `gen`).  On a ROCm device with
+    ahead=True (no --target-kl early stop, so every epoch's permutation is drawn), epoch e + 1's is drawn
+    on a side stream while epoch e's minibatches run, overlapping the GEMMs instead of preceding the
     epoch's first minibatch.  The generator is consumed in the same order: the same permutations."""
 
     def __init__(self, batch: int, device, gen, epochs: int, ahead: bool = True):
@@ -1004,14 +1007,22 @@ class EpochPermutations:
             self.side = _SIDE_STREAMS.setdefault(key, torch.cuda.Stream(device=self.device))
         self.pending = None
 
+    def _perm(self):
+        if self.device.type != "cuda" or not RANDPERM_HIP or self.batch >= 2 ** 31:
+            return torch.randperm(self.batch, device=self.device, generator=self.gen)
+        # ROCm: vss_randperm from one seed drawn from gen (the same distribution as torch.randperm's,
+        # 4 radix passes instead of 8 plus a duplicate-key pass)
+        seed = torch.randint(-2 ** 63, 2 ** 63 - 1, (1,), device=self.device, dtype=torch.int64, generator=self.gen)
+        return randperm(self.batch, seed)
+
     def _draw(self):
         self.left -= 1
         if self.side is None:
-            return torch.randperm(self.batch, device=self.device, generator=self.gen), None
+            return self._perm(), None
         main = torch.cuda.current_stream(self.device)
         self.side.wait_stream(main)  # the generator's state and the allocator: after what main queued so far
         with torch.cuda.stream(self.side):
-            p = torch.randperm(self.batch, device=self.device, generator=self.gen)
+            p = self._perm()
             ev = torch.cuda.Event()
             ev.record(self.side)
         return p, ev

@@ -186,6 +186,22 @@ def ppo_loss_fused_finish(actor_stats, critic_stats, rows: int, logstd, ent_coef
     return loss, stats
 
 
+def randperm(n: int, seed: torch.Tensor) -> torch.Tensor:
+    """A uniformly random permutation of [0, n) (int64, on seed's device) determined by seed, one int64 on
+    the ROCm device drawn from the update's generator (vss_randperm: 32 random bits per index, a stable
+    4-pass radix sort) -- torch.randperm(n) of ppo…:309 in a quarter of its sort passes' key bytes."""
+    if seed.dtype != torch.int64 or seed.numel() != 1 or seed.device.type != "cuda" or not 0 < n < 2 ** 31:
+        raise ValueError(f"randperm: n in (0, 2^31) and a one-element int64 ROCm seed, got {n}, {seed.dtype} "
+                         f"{tuple(seed.shape)} on {seed.device}")
+    lib = N.load()
+    nb = int(lib.vss_randperm_scratch_bytes(n))
+    scratch = torch.empty(nb, dtype=torch.uint8, device=seed.device)
+    out = torch.empty(n, dtype=torch.int64, device=seed.device)
+    N.check(lib.vss_randperm(N.stream_of(seed.device), n, seed.data_ptr(), out.data_ptr(), scratch.data_ptr(), nb),
+            "vss_randperm")
+    return out
+
+
 def minibatch_gather_parts(mb: int) -> int:
     """Rows of the (sum, sum of squares) parts minibatch_gather writes for mb minibatch rows."""
     return int(N.load().vss_minibatch_gather_parts(mb))

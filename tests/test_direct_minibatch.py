@@ -12,7 +12,7 @@ import torch
 import ppo_continuous_action_isaacgym as P
 from test_ppo import _args, _synthetic_batch, make_agent
 from vss_amd.loss import (N_ACT, adv_part_sum, minibatch_gather, minibatch_gather_parts, ppo_loss, ppo_loss_direct,
-                          ppo_loss_fused_finish)
+                          ppo_loss_fused_finish, randperm)
 from vss_amd.update import (linear_tanh_loss_x6, linear_tanh_loss_x6_ok, linear_tanh_out_x6, output_backward,
                             output_backward_direct, output_backward_direct_ok)
 
@@ -228,3 +228,37 @@ def test_direct_minibatch_matches_autograd_path_gpu(n, nmb, act_dim, norm_adv, c
     _, st2 = P.direct_minibatch(agent, args, rows.obs, rows.act, rows.logp, rows.adv, *src, rows.ret, rows.val)
     assert all(torch.equal(a, b) for a, b in zip(got, _grads(agent)))
     assert all(float(a) == float(b) for a, b in zip(st1, st2))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 1000, 262080, 8388608])
+def test_randperm_is_a_seeded_permutation_gpu(n):
+    """vss_randperm: a permutation of [0, n) (sorted = arange), the same for the same seed, different
+    for another; at 8,388,608 (the SA batch) the scratch and the 4-pass sort hold."""
+    dev = "cuda"
+    s1 = torch.tensor([1234567], dtype=torch.int64, device=dev)
+    s2 = torch.tensor([-987654321], dtype=torch.int64, device=dev)
+    p1, p1b, p2 = randperm(n, s1), randperm(n, s1), randperm(n, s2)
+    assert p1.dtype == torch.int64 and p1.shape == (n,)
+    assert torch.equal(torch.sort(p1).values, torch.arange(n, device=dev))
+    assert torch.equal(p1, p1b)
+    if n >= 1000:
+        assert not torch.equal(p1, p2) and not torch.equal(p1, torch.arange(n, device=dev))
+
+
+@pytest.mark.gpu
+def test_randperm_is_uniform_gpu():
+    """Uniformity of vss_randperm over seeds: for n = 8, 10,000 seeds, every (element, position) count
+    within 5 sigma of 1,250, and the fixed-point count's mean near 1 (a uniform permutation's)."""
+    n, draws = 8, 10000
+    seeds = torch.randint(-2 ** 62, 2 ** 62, (draws,), generator=torch.Generator().manual_seed(5))
+    counts = torch.zeros(n, n, dtype=torch.int64)
+    fixed = 0
+    for s in seeds.tolist():
+        p = randperm(n, torch.tensor([s], dtype=torch.int64, device="cuda")).cpu()
+        counts[torch.arange(n), p] += 1
+        fixed += int((p == torch.arange(n)).sum())
+    expect = draws / n
+    sigma = (draws * (1 / n) * (1 - 1 / n)) ** 0.5
+    assert float((counts.double() - expect).abs().max()) < 5 * sigma, counts
+    assert abs(fixed / draws - 1.0) < 0.05

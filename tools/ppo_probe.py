@@ -20,6 +20,8 @@ if os.environ.get("PROBE_ENV", "0") == "1":
     for _ in range(300):
         env.step(a)
     torch.cuda.synchronize()
+if os.environ.get("PROBE_RANDPERM") == "arange":  # upper bound of a free permutation: no shuffle at all
+    torch.randperm = lambda n, device=None, generator=None, **kw: torch.arange(n, device=device)  # noqa: E731
 args = P.parse_args(["--env-id", os.environ.get("ENV_ID", "sa"), "--num-envs", os.environ.get("NUM_ENVS", "65536"), "--num-updates", os.environ.get("UPDATES", "3"),
                      "--log", os.environ.get("PROBE_LOG", "false"), "--seed", "1", "--save-path", "/tmp/runs"])
 _, hist = P.train(args)

@@ -16,7 +16,8 @@ import os
 import torch  # noqa: F401  (loads torch's HIP runtime before the library resolves it)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libvss_amd.so")
+# VSS_LIB_PATH: a variant build of the same sources for A/B measurements (tools/), never the product
+LIB_PATH = os.environ.get("VSS_LIB_PATH") or os.path.join(HERE, "libvss_amd.so")
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "vss.h")
 

@@ -53,6 +53,18 @@ elif mode == "bwd":
     wn = torch.randn(k, n, device="cuda", generator=g) / k ** 0.5
     y = torch.tanh(torch.randn(rows, n, device="cuda", generator=g))
     fn = lambda: linear_tanh_backward_x6(gn, wn, y)  # noqa: E731
+elif mode == "loss":  # the actor's last hidden layer with the output layer and loss (EPI_LOSS_A), k_out 2
+    from vss_amd.update import linear_tanh_loss_x6, weight_planes  # noqa: E402
+    x = torch.tanh(torch.randn(rows, k, device="cuda", generator=g))
+    w = torch.randn(n, k, device="cuda", generator=g) / k ** 0.5
+    b = torch.zeros(n, device="cuda")
+    wo, bo = torch.randn(2, n, device="cuda", generator=g) / 16, torch.zeros(2, device="cuda")
+    pl = weight_planes([(w, False)])[0]
+    act = torch.randn(rows, 2, device="cuda", generator=g) * 0.3
+    logp, adv = torch.randn(rows, device="cuda", generator=g) - 1, torch.randn(rows, device="cuda", generator=g)
+    ls = torch.zeros(1, 2, device="cuda")
+    fn = lambda: linear_tanh_loss_x6(x, w, b, wo, bo, rows, True, planes=pl, act=act, logp=logp, adv=adv,  # noqa: E731
+                                     logstd=ls)
 else:
     gz = torch.randn(rows, n, device="cuda", generator=g)
     x = torch.tanh(torch.randn(rows, k, device="cuda", generator=g))

@@ -42,6 +42,12 @@ def main():
         if mode == "bwd":  # grad_next (rows, k) in, y (rows, n) in, grad (rows, n) out
             algo = 4.0 * rows * (k + 2 * n)
             shape = f"backward {n}<-{k}"
+        elif mode == "fwd":  # x (rows, k) in, y (rows, n) out
+            algo = 4.0 * rows * (k + n)
+            shape = f"forward {k}->{n}"
+        elif mode == "loss":  # x (rows, k) + action (2) / logprob / advantage per row in, gz (rows, n) out
+            algo = 4.0 * rows * (k + n + 4)
+            shape = f"last layer + loss {k}->{n}"
         else:  # grad (rows, n) and x (rows, k) in; the (splits, n, k) partials out are not counted
             algo = 4.0 * rows * (k + n)
             shape = f"weight gradient {n}x{k}"

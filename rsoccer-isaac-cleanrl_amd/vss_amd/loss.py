@@ -171,6 +171,8 @@ def ppo_loss_fused_finish(actor_stats, critic_stats, rows: int, logstd, ent_coef
     for t in (actor_stats, critic_stats, logstd, grad_logstd, grad_mean_bias, grad_value_bias):
         if t.dtype != torch.float32 or t.device != actor_stats.device or not t.is_contiguous():
             raise ValueError("ppo_loss_fused_finish: contiguous fp32 tensors on one device")
+    if actor_stats.device.type != "cuda":
+        raise ValueError("ppo_loss_fused_finish: ROCm tensors only (no CPU path)")
     if n_act not in (1, 2) or actor_stats.dim() != 2 or actor_stats.shape[1] != 32 or critic_stats.dim() != 2 \
             or critic_stats.shape[1] != 32 or grad_logstd.numel() != n_act or grad_mean_bias.numel() != n_act \
             or grad_value_bias.numel() != 1 or rows <= 0:

@@ -285,7 +285,7 @@ def linear_tanh_loss_x6(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, w_out
     n, k_out = w.shape[0], w_out.shape[0]
     _x6_check("vss_linear_tanh_loss_bf16x6", w.shape == (n, k) and b.shape == (n,) and w_out.shape == (k_out, n)
               and b_out.shape == (k_out,) and 0 < rows <= rows_pad and linear_tanh_loss_x6_ok(rows_pad, k, n, k_out)
-              and (not actor or k_out == 2 or k_out == 1) and (actor or k_out == 1), x, w, b, w_out)
+              and (actor or k_out == 1), x, w, b, w_out)
     rows_t = (act, logp, adv, logstd) if actor else (ret,) + ((val,) if clip_vloss else ())
     for t in rows_t:
         if t is None or t.dtype != torch.float32 or t.device != x.device or not t.is_contiguous():

@@ -33,6 +33,23 @@ def test_fused_loss_shapes_cpu():
     assert not linear_tanh_loss_x6_ok(4096, 256, 512, 2)
 
 
+def test_fused_loss_and_randperm_refuse_cpu_inputs_cpu():
+    """No CPU fallback: the fused loss launch, its finish and vss_randperm refuse CPU tensors (and bad
+    shapes) before touching the library."""
+    x, w, b = torch.zeros(256, 256), torch.zeros(256, 256), torch.zeros(256)
+    wo, bo = torch.zeros(2, 256), torch.zeros(2)
+    with pytest.raises(ValueError):
+        linear_tanh_loss_x6(x, w, b, wo, bo, 256, True)
+    with pytest.raises(ValueError):  # 6 outputs: outside the fused shapes
+        linear_tanh_loss_x6(x, w, b, torch.zeros(6, 256), torch.zeros(6), 256, True)
+    for gvb in (torch.zeros(1), torch.zeros(3)):  # CPU tensors; a bad shape
+        with pytest.raises(ValueError):
+            ppo_loss_fused_finish(torch.zeros(4, 32), torch.zeros(4, 32), 256, torch.zeros(1, 2), 0.0, 0.5,
+                                  torch.zeros(1, 2), torch.zeros(2), gvb)
+    with pytest.raises(ValueError):
+        randperm(10, torch.zeros(1, dtype=torch.int64))
+
+
 def test_direct_minibatch_not_for_cpu_or_amp():
     """direct_minibatch_ok: FlatGrads-owned GPU gradients, fp32 networks -- CPU agents and --amp keep the
     autograd path."""

@@ -155,7 +155,8 @@ def test_ppo_loss_direct_matches_loss_on_summed_outputs_gpu(norm, clip_vloss):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("rows,rows_pad,n_act,norm,clip_vloss", [
-    (131040, 131072, 2, True, False), (65536, 65536, 2, True, True), (1000, 1024, 1, False, True)])
+    (131040, 131072, 2, True, False), (65536, 65536, 2, True, True), (1000, 1024, 1, False, True),
+    (300, 512, 2, True, True), (1, 256, 1, False, False)])
 def test_fused_loss_matches_separate_launches_gpu(rows, rows_pad, n_act, norm, clip_vloss):
     """vss_linear_tanh_loss_bf16x6 (actor and critic) + vss_ppo_loss_fused_finish = the separate launches
     direct_minibatch otherwise runs (vss_linear_tanh_out_bf16x6 with parts, vss_ppo_loss_direct,

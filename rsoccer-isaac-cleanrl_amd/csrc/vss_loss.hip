@@ -233,25 +233,36 @@ __global__ __launch_bounds__(kThreads) void loss_finish_kernel(int blocks, const
 // the fused loss epilogue's per-block sums (vss_gemm_x6.hip EPI_LOSS_A / EPI_LOSS_C, vlossrow::kBlockStats
 // layout) -> the loss, its statistics, the log-std gradient and the output biases' gradients, as
 // loss_finish_kernel<NA, true> forms them
+constexpr int kFinishThreads = 1024;
 template <int NA>
-__global__ __launch_bounds__(kThreads) void fused_finish_kernel(int actor_blocks, const float* __restrict__ actor,
+__global__ __launch_bounds__(kFinishThreads) void fused_finish_kernel(int actor_blocks, const float* __restrict__ actor,
                                                                 int critic_blocks, const float* __restrict__ critic,
                                                                 const float* __restrict__ logstd, float ent_coef,
                                                                 float vf_coef, float n, float inv_n,
                                                                 float* __restrict__ g_logstd, float* __restrict__ loss_out,
                                                                 float* __restrict__ stats, float* __restrict__ db_mean,
                                                                 float* __restrict__ db_value) {
-  constexpr int S = vlossrow::kBlockStats;
+  // thread t: quantity k = t % 64 (actor's 32, then the critic's), block chunk c = t / 64 of kFinishThreads / 64:
+  // its blocks c, c + 16, ... summed with all loads in flight at once, then the 16 chunk sums in order
+  constexpr int S = vlossrow::kBlockStats, CH = kFinishThreads / 64;
+  __shared__ float part[CH][2 * S];
   __shared__ float tot[2 * S];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int k = wv; k < 2 * S; k += kThreads / 64) {
+  {
+    const int k = threadIdx.x & 63, ch = threadIdx.x >> 6;
     const bool c = k >= S;
     const float* p = c ? critic : actor;
     const int blocks = c ? critic_blocks : actor_blocks, kk = c ? k - S : k;
     float s = 0.f;
-    for (int b = lane; b < blocks; b += 64) s += p[(int64_t)b * S + kk];
-    s = wave_sum(s);
-    if (lane == 0) tot[k] = s;
+#pragma unroll 8
+    for (int b = ch; b < blocks; b += CH) s += p[(int64_t)b * S + kk];
+    part[ch][k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * S) {
+    float s = part[0][threadIdx.x];
+#pragma unroll
+    for (int ch = 1; ch < CH; ++ch) s += part[ch][threadIdx.x];
+    tot[threadIdx.x] = s;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -527,7 +538,7 @@ int vss_ppo_loss_fused_finish(void* stream, int64_t rows, int32_t n_act, int64_t
   if (rows <= 0 || actor_blocks < 1 || critic_blocks < 1 || !actor_stats || !critic_stats || !logstd || !grad_logstd ||
       !grad_mean_bias || !grad_value_bias || !loss_out || !stats_out)
     return VSS_E_ARG;
-  const dim3 grid(1), block(vloss::kThreads);
+  const dim3 grid(1), block(vloss::kFinishThreads);
   const float n = (float)rows, inv_n = 1.0f / (float)rows;
   if (n_act == 1)
     hipLaunchKernelGGL((vloss::fused_finish_kernel<1>), grid, block, 0, (hipStream_t)stream, (int)actor_blocks,

@@ -280,3 +280,29 @@ def test_randperm_is_uniform_gpu():
     sigma = (draws * (1 / n) * (1 - 1 / n)) ** 0.5
     assert float((counts.double() - expect).abs().max()) < 5 * sigma, counts
     assert abs(fixed / draws - 1.0) < 0.05
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hip", [True, False])
+def test_epoch_permutations_gpu(hip, monkeypatch):
+    """EpochPermutations on the GPU (side stream, drawn one epoch ahead): every epoch a permutation of the
+    batch, the same sequence for the same generator seed; with VSS_RANDPERM=torch exactly torch.randperm's
+    sequence from that generator."""
+    monkeypatch.setattr(P, "RANDPERM_HIP", hip)
+    batch, epochs = 100000, 4
+
+    def draw(seed):
+        gen = torch.Generator(device="cuda").manual_seed(seed)
+        perms = P.EpochPermutations(batch, "cuda", gen, epochs)
+        return [perms.next().clone() for _ in range(epochs)]
+
+    a, b, c = draw(5), draw(5), draw(6)
+    ar = torch.arange(batch, device="cuda")
+    for p in a:
+        assert torch.equal(torch.sort(p).values, ar)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
+    assert not torch.equal(a[0], c[0]) and not torch.equal(a[0], a[1])
+    if not hip:
+        gen = torch.Generator(device="cuda").manual_seed(5)
+        want = [torch.randperm(batch, device="cuda", generator=gen) for _ in range(epochs)]
+        assert all(torch.equal(x, y) for x, y in zip(a, want))

@@ -16,8 +16,24 @@ import os
 import torch  # noqa: F401  (loads torch's HIP runtime before the library resolves it)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# VSS_LIB_PATH: a variant build of the same sources for A/B measurements (tools/), never the product
-LIB_PATH = os.environ.get("VSS_LIB_PATH") or os.path.join(HERE, "libvss_amd.so")
+TOOLS = os.path.join(os.path.dirname(os.path.dirname(HERE)), "tools")
+
+
+def _lib_path() -> str:
+    """The in-tree libvss_amd.so; VSS_LIB_PATH may name a variant build of the same sources for A/B
+    measurements, and only one under the repository's tools/ (it still has to pass the source-stamp check)."""
+    alt = os.environ.get("VSS_LIB_PATH")
+    if not alt:
+        return os.path.join(HERE, "libvss_amd.so")
+    alt = os.path.realpath(alt)
+    if not alt.startswith(os.path.realpath(TOOLS) + os.sep):
+        raise RuntimeError(f"VSS_LIB_PATH={alt}: only variant builds under {TOOLS} are accepted")
+    import warnings
+    warnings.warn(f"libvss_amd: loading the variant build {alt} (VSS_LIB_PATH)", RuntimeWarning)
+    return alt
+
+
+LIB_PATH = _lib_path()
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "vss.h")
 

@@ -35,12 +35,15 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "rsoccer-isaac-cleanrl_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 
-# before torch initialises the GPU: the PPO legs run with ROCm's graph packet capture off
-# (ppo_continuous_action_isaacgym.py disable_graph_packet_capture; the captured minibatch also checks itself)
-os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
+
+# before anything initialises the GPU: the PPO legs run with ROCm's graph packet capture off, and the
+# captured minibatch checks that the runtime started that way (vss_amd.minibatch; it also checks itself)
+from vss_amd.minibatch import disable_graph_packet_capture  # noqa: E402
+
+disable_graph_packet_capture()
 
 METRIC = "env-steps/s (num_envs×horizon) at 65 536 envs; PPO wall-clock to 1e8 steps"
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip table (spec)
@@ -306,6 +309,7 @@ def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
     gradients are averaged by one flat all-reduce per minibatch (RCCL), so the figures here are
     max-over-ranks times and whole-job (all-rank) env-steps."""
     import ppo_continuous_action_isaacgym as P
+    from vss_amd import minibatch as MB, mlp as M
     args = P.parse_args(["--env-id", "sa", "--num-envs", str(n_envs), "--num-updates", str(updates),
                          "--log", "false", "--seed", "1"])
     t0 = time.perf_counter()
@@ -332,9 +336,9 @@ def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
             "num_minibatches": args.num_minibatches, "dtype": "f32",
             "update_gemm": {"x6": "fp32 arithmetic on the bf16 matrix cores (exact 3-way bf16 split, six partial "
                                   "products, fp32 accumulation; csrc/vss_gemm_x6.hip)",
-                            "fp32": "fp32 MFMA (csrc/vss_update.hip)"}.get(P.UPDATE_GEMM, P.UPDATE_GEMM),
+                            "fp32": "fp32 MFMA (csrc/vss_update.hip)"}.get(M.UPDATE_GEMM, M.UPDATE_GEMM),
             "update_minibatch": ("one captured HIP graph per minibatch (forward, losses, backward), "
-                                 f"rows padded to {P.MLP_ROW_PAD}, replay {P.GRAPH_CHECK_REPLAY} checked against eager"
+                                 f"rows padded to {MB.MLP_ROW_PAD}, replay {MB.GRAPH_CHECK_REPLAY} checked against eager"
                                  if args.update_graph else "eager"),
             "graph_packet_capture_env": os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "<unset>"),
             "gradient_exchange": ("one flat fp32 all-reduce per minibatch "

@@ -485,10 +485,14 @@ int vss_ppo_loss_fused_finish(void* stream, int64_t rows, int32_t n_act, int64_t
 /* vss_randperm: the epoch's minibatch permutation (ppo…:309, torch.randperm(batch)): out (n,) int64 a
  * uniformly random permutation of [0, n) determined by seed[0] (one int64 on the device, drawn from the
  * update's generator), 0 < n < 2^31.  scratch: vss_randperm_scratch_bytes(n) bytes (-1 for a bad n),
- * 256-B aligned.  Each index gets 32 random bits (splitmix64 of seed and index); a stable radix sort on
- * them (4 passes, hipcub) orders the indices; ties keep index order. */
+ * 256-B aligned.  Each index gets 32 random bits (splitmix64 of seed and index); a radix sort on them
+ * (4 passes, hipcub) orders the indices, and every run of tied bits is then shuffled (Fisher-Yates from a
+ * second stream), so the permutation is uniform.  vss_randperm_bits: the same with key_bits (1..32) random
+ * bits per index -- fewer bits force ties (the tie pass's test entry); vss_randperm = key_bits 32. */
 int64_t vss_randperm_scratch_bytes(int64_t n);
 int vss_randperm(void* stream, int64_t n, const int64_t* seed, int64_t* out, void* scratch, int64_t scratch_bytes);
+int vss_randperm_bits(void* stream, int64_t n, int32_t key_bits, const int64_t* seed, int64_t* out, void* scratch,
+                      int64_t scratch_bytes);
 int64_t vss_minibatch_gather_parts(int64_t mb);
 int vss_minibatch_gather(void* stream, int64_t mb, int64_t rows_pad, int64_t batch, const int64_t* inds, int64_t obs_w,
                          int64_t act_w, const float* b_obs, const float* b_act, const float* b_logp, const float* b_adv,
@@ -504,8 +508,9 @@ int vss_adv_part_sum(void* stream, int32_t nparts, const double* part, double* o
  *
  * vss_grad_sq_partials: partial[b] = sum of grad[i]^2 over block b's chunk, b < count =
  *   vss_grad_sq_partials_count(n) (<= 1024; -1 for n <= 0); fixed order (deterministic).
- * vss_adam_step_clipped: norm = sqrt(sum of the nparts partials); with max_norm > 0 the gradients are
- *   scaled in place by min(1, max_norm / (norm + 1e-6)) (clip_grad_norm_); then Adam's step `step`
+ * vss_adam_step_clipped: norm = sqrt(sum of the nparts partials); with max_norm >= 0 the gradients are
+ *   scaled in place by min(1, max_norm / (norm + 1e-6)) (clip_grad_norm_: max_norm 0 zeroes them, as
+ *   torch's does), with max_norm < 0 they are left alone (no clip requested); then Adam's step `step`
  *   (>= 1, the count after this step) with torch's fused-Adam arithmetic: m = b1 m + (1 - b1) g,
  *   v = b2 v + (1 - b2) g^2, p -= lr / (1 - b1^step) * m / (sqrt(v) / sqrt(1 - b2^step) + eps).
  *   norm_out (1 float, may be NULL) receives the pre-clip norm.  All buffers n fp32 elements.

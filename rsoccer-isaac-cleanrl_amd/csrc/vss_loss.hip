@@ -445,23 +445,50 @@ static int64_t gather_scalar_blocks(int64_t mb) {
 
 // ---- the epoch's minibatch permutation (ppo…:309, torch.randperm(batch)): a uniformly random
 // permutation from one 64-bit seed drawn from the update's generator.  Each index i gets the key
-// (32 random bits << 32) | i, with the random bits from splitmix64 of (seed, i); a stable radix sort on
-// the high 32 bits (4 passes) orders the indices by their random bits (ties, ~n^2 / 2^33 pairs, keep index
-// order), and the low 32 bits of the sorted keys are the permutation, written in place as int64.  Against
-// torch's randperm (64-bit keys: 8 passes, plus its duplicate-key pass) half the sort traffic.
+// (b random bits << (64 - b)) | i (b = 32 in the product), with the random bits from splitmix64 of (seed, i); a
+// radix sort on the high bits (4 passes for b = 32) orders the indices by their random bits.  Indices whose
+// random bits tie (~n^2 / 2^33 pairs at b = 32) would keep index order after the stable sort; a pass over
+// the sorted keys shuffles every such run (Fisher-Yates from a second splitmix64 stream), so the order within
+// a run is uniform and independent of the keys, and the permutation is uniform -- as torch.randperm, which
+// sorts 64-bit keys (8 passes) and then shuffles its duplicate-key runs the same way.  The low 32 bits of the
+// sorted keys are the permutation, written in place as int64.
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
 
-__global__ __launch_bounds__(kThreads) void perm_keys_kernel(int64_t n, const int64_t* __restrict__ seed,
+__global__ __launch_bounds__(kThreads) void perm_keys_kernel(int64_t n, int key_bits, const int64_t* __restrict__ seed,
                                                              uint64_t* __restrict__ keys) {
   const uint64_t s = (uint64_t)seed[0];
+  const uint64_t mask = ~0ull << (64 - key_bits);  // the top key_bits of the random word, in bits 32 + ..
   const int64_t stride = (int64_t)gridDim.x * kThreads;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
     const uint64_t r = splitmix64(s + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull);
-    keys[i] = (r & 0xFFFFFFFF00000000ull) | (uint64_t)i;
+    keys[i] = (r & mask) | (uint64_t)i;
+  }
+}
+
+// the sorted keys' tied runs (equal high halves) shuffled in place: the thread at a run's first position
+// (its left neighbour differs, its right one is equal) walks the run and Fisher-Yates-shuffles its low halves.
+// The high halves never change, so the neighbour tests read the same values whatever the other runs' threads
+// have written so far; runs are disjoint, so every entry has one writer.
+__global__ __launch_bounds__(kThreads) void perm_ties_kernel(int64_t n, const int64_t* __restrict__ seed,
+                                                             uint64_t* __restrict__ keys) {
+  const uint64_t s = (uint64_t)seed[0] ^ 0xD1B54A32D192ED03ull;  // a stream apart from the keys'
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i + 1 < n; i += stride) {
+    const uint64_t hi = keys[i] >> 32;
+    if ((keys[i + 1] >> 32) != hi || (i > 0 && (keys[i - 1] >> 32) == hi)) continue;
+    int64_t end = i + 2;
+    while (end < n && (keys[end] >> 32) == hi) ++end;
+    for (int64_t t = end - 1; t > i; --t) {  // position t takes a uniform pick among [i, t]
+      const uint64_t r = splitmix64(s + (uint64_t)(t + 1) * 0x9E3779B97F4A7C15ull);
+      const int64_t j = i + (int64_t)(r % (uint64_t)(t - i + 1));
+      const uint64_t a = keys[t], b = keys[j];
+      keys[t] = b;
+      keys[j] = a;
+    }
   }
 }
 
@@ -560,23 +587,30 @@ int64_t vss_randperm_scratch_bytes(int64_t n) {
   return ((n * 8 + 255) / 256) * 256 + (int64_t)sort;
 }
 
-int vss_randperm(void* stream, int64_t n, const int64_t* seed, int64_t* out, void* scratch, int64_t scratch_bytes) {
+int vss_randperm_bits(void* stream, int64_t n, int32_t key_bits, const int64_t* seed, int64_t* out, void* scratch,
+                      int64_t scratch_bytes) {
   const int64_t need = vss_randperm_scratch_bytes(n);
-  if (need < 0 || !seed || !out || !scratch || scratch_bytes < need || (reinterpret_cast<uintptr_t>(scratch) & 255) ||
-      (reinterpret_cast<uintptr_t>(out) & 7))
+  if (need < 0 || key_bits < 1 || key_bits > 32 || !seed || !out || !scratch || scratch_bytes < need ||
+      (reinterpret_cast<uintptr_t>(scratch) & 255) || (reinterpret_cast<uintptr_t>(out) & 7))
     return VSS_E_ARG;
   uint64_t* keys = static_cast<uint64_t*>(scratch);
   char* temp = static_cast<char*>(scratch) + ((n * 8 + 255) / 256) * 256;
   size_t temp_bytes = (size_t)(scratch_bytes - ((n * 8 + 255) / 256) * 256);
   const hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)vloss::perm_grid(n)), block(vloss::kThreads);
-  hipLaunchKernelGGL(vloss::perm_keys_kernel, grid, block, 0, st, n, seed, keys);
+  hipLaunchKernelGGL(vloss::perm_keys_kernel, grid, block, 0, st, n, (int)key_bits, seed, keys);
   if (hipGetLastError() != hipSuccess) return VSS_E_LAUNCH;
-  if (hipcub::DeviceRadixSort::SortKeys(temp, temp_bytes, keys, reinterpret_cast<uint64_t*>(out), (int)n, 32, 64, st) !=
-      hipSuccess)
+  if (hipcub::DeviceRadixSort::SortKeys(temp, temp_bytes, keys, reinterpret_cast<uint64_t*>(out), (int)n,
+                                        64 - key_bits, 64, st) != hipSuccess)
     return VSS_E_LAUNCH;
+  hipLaunchKernelGGL(vloss::perm_ties_kernel, grid, block, 0, st, n, seed, reinterpret_cast<uint64_t*>(out));
+  if (hipGetLastError() != hipSuccess) return VSS_E_LAUNCH;
   hipLaunchKernelGGL(vloss::perm_index_kernel, grid, block, 0, st, n, reinterpret_cast<uint64_t*>(out));
   return hipGetLastError() == hipSuccess ? VSS_OK : VSS_E_LAUNCH;
+}
+
+int vss_randperm(void* stream, int64_t n, const int64_t* seed, int64_t* out, void* scratch, int64_t scratch_bytes) {
+  return vss_randperm_bits(stream, n, 32, seed, out, scratch, scratch_bytes);
 }
 
 int64_t vss_minibatch_gather_parts(int64_t mb) { return mb <= 0 ? -1 : vloss::gather_scalar_blocks(mb); }

@@ -75,7 +75,8 @@ __global__ __launch_bounds__(kThreads) void adam_step_kernel(int64_t n, int32_t 
   const float sq = block_sum(s, red);
   const float norm = sqrtf(sq);
   float coef = 1.f;
-  if (max_norm > 0.f) {  // clip_grad_norm_: clip_coef = max_norm / (total_norm + 1e-6), clamped to 1
+  const bool clip = max_norm >= 0.f;  // < 0: no clip requested (0 is a clip to zero, as clip_grad_norm_'s)
+  if (clip) {  // clip_grad_norm_: clip_coef = max_norm / (total_norm + 1e-6), clamped to 1
     const float c = max_norm / (norm + 1e-6f);
     coef = c < 1.f ? c : 1.f;
   }
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(kThreads) void adam_step_kernel(int64_t n, int32_t 
   const int64_t stride = (int64_t)gridDim.x * kThreads;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
     float gi = g[i];
-    if (max_norm > 0.f) {
+    if (clip) {
       gi = gi * coef;
       g[i] = gi;
     }

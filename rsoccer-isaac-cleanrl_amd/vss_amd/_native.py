@@ -62,7 +62,7 @@ EXPORTED = ("vss_abi_version", "vss_source_hash", "vss_error_string", "vss_step"
             "vss_output_backward_direct_chunks", "vss_output_backward_direct", "vss_ppo_loss_direct_scratch_floats",
             "vss_ppo_loss_direct", "vss_minibatch_gather_parts", "vss_minibatch_gather", "vss_adv_part_sum",
             "vss_first_layer_bf16x6", "vss_linear_tanh_loss_blocks_bf16x6", "vss_linear_tanh_loss_bf16x6",
-            "vss_ppo_loss_fused_finish", "vss_randperm_scratch_bytes", "vss_randperm")
+            "vss_ppo_loss_fused_finish", "vss_randperm_scratch_bytes", "vss_randperm", "vss_randperm_bits")
 
 
 class VssParams(ctypes.Structure):
@@ -244,6 +244,8 @@ def load() -> ctypes.CDLL:
     L.vss_randperm_scratch_bytes.restype = i64
     L.vss_randperm.argtypes = [P, i64, P, P, P, i64]
     L.vss_randperm.restype = ctypes.c_int
+    L.vss_randperm_bits.argtypes = [P, i64, ctypes.c_int32, P, P, P, i64]
+    L.vss_randperm_bits.restype = ctypes.c_int
     if L.vss_abi_version() != ABI_VERSION:
         raise NativeError(f"libvss_amd ABI {L.vss_abi_version()} != expected {ABI_VERSION}")
     _lib = L

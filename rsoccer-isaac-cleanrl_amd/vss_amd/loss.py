@@ -188,19 +188,21 @@ def ppo_loss_fused_finish(actor_stats, critic_stats, rows: int, logstd, ent_coef
     return loss, stats
 
 
-def randperm(n: int, seed: torch.Tensor) -> torch.Tensor:
+def randperm(n: int, seed: torch.Tensor, key_bits: int = 32) -> torch.Tensor:
     """A uniformly random permutation of [0, n) (int64, on seed's device) determined by seed, one int64 on
-    the ROCm device drawn from the update's generator (vss_randperm: 32 random bits per index, a stable
-    4-pass radix sort) -- torch.randperm(n) of ppo…:309 in a quarter of its sort passes' key bytes."""
-    if seed.dtype != torch.int64 or seed.numel() != 1 or seed.device.type != "cuda" or not 0 < n < 2 ** 31:
-        raise ValueError(f"randperm: n in (0, 2^31) and a one-element int64 ROCm seed, got {n}, {seed.dtype} "
-                         f"{tuple(seed.shape)} on {seed.device}")
+    the ROCm device drawn from the update's generator (vss_randperm: 32 random bits per index, a 4-pass
+    radix sort, every run of tied bits shuffled) -- torch.randperm(n) of ppo…:309 in half its sort passes.
+    key_bits < 32 draws fewer random bits per index, forcing ties (tests of the tie pass)."""
+    if seed.dtype != torch.int64 or seed.numel() != 1 or seed.device.type != "cuda" or not 0 < n < 2 ** 31 \
+            or not 1 <= key_bits <= 32:
+        raise ValueError(f"randperm: n in (0, 2^31), key_bits in [1, 32] and a one-element int64 ROCm seed, got {n}, "
+                         f"{key_bits}, {seed.dtype} {tuple(seed.shape)} on {seed.device}")
     lib = N.load()
     nb = int(lib.vss_randperm_scratch_bytes(n))
     scratch = torch.empty(nb, dtype=torch.uint8, device=seed.device)
     out = torch.empty(n, dtype=torch.int64, device=seed.device)
-    N.check(lib.vss_randperm(N.stream_of(seed.device), n, seed.data_ptr(), out.data_ptr(), scratch.data_ptr(), nb),
-            "vss_randperm")
+    N.check(lib.vss_randperm_bits(N.stream_of(seed.device), n, int(key_bits), seed.data_ptr(), out.data_ptr(),
+                                  scratch.data_ptr(), nb), "vss_randperm_bits")
     return out
 
 

@@ -204,3 +204,41 @@ class FusedPolicy:
     @torch.no_grad()
     def actor_mean(self, obs):
         return self._run(obs, True, want_mean=True)[4]
+
+
+class TerminalValues:
+    """next_values[t] = critic(terminal_obs_t) (ppo…:272) for the fused rollout, in ONE masked critic
+    pass after the rollout instead of a critic pass per step.  For a field that did not reset at
+    step t the terminal observation IS next_obs_t, whose value the next step computes (values[t+1],
+    or critic(next_obs) after the last step), so only the reset rows need the terminal pass; the
+    critic does not change within a rollout, so one pass over all T x E recorded terminal
+    observations, masked by the dones, gives the same values.  (A masked pass per step cost
+    ~0.22 ms however few rows reset -- one wave's serial walk through the critic.)  Memory: the
+    (T, E, obs) fp32 copy of the terminal observations, 1.7 GB at T = 128, E = 65,536 and 5.1 GB
+    for DMA at 196,608 agent rows (<= 2 % of one MI355X's 288 GB)."""
+
+    def __init__(self, T, E, obs_shape, device):
+        self.T, self.E = T, E
+        self.term_obs = torch.zeros((T, E) + tuple(obs_shape), device=device)
+        self.term_mask = torch.zeros((T, E), device=device, dtype=torch.long)
+        self.term_values = torch.zeros((T, E), device=device)
+
+    def record(self, step, terminal_obs, done):
+        self.term_obs[step].copy_(terminal_obs.reshape(self.term_obs.shape[1:]))
+        self.term_mask[step].copy_(done)
+
+    def next_values(self, fused, values, next_dones, next_obs):
+        """(T, E) next_values: the masked terminal pass where a field reset, else values[t + 1].  When
+        the rollout's values come from the GEMM chain (FusedPolicy.chain_active), the reset rows are
+        gathered and evaluated by the same chain (one host sync for their count, once per rollout), so
+        next_values stays exactly critic(terminal_obs) of one evaluator."""
+        if fused.chain_active(self.E):
+            idx = self.term_mask.view(-1).nonzero().squeeze(1)
+            tv = self.term_values.view(-1)
+            if idx.numel():
+                tv.index_copy_(0, idx, fused.values_chain(self.term_obs.view(self.T * self.E, -1).index_select(0, idx))
+                               .view(-1))
+        else:
+            fused.get_value_masked(self.term_obs, self.term_mask, self.term_values.view(self.T * self.E, 1))
+        v_last = fused.get_value(next_obs).view(1, self.E)
+        return torch.where(next_dones.bool(), self.term_values, torch.cat([values[1:], v_last], 0))

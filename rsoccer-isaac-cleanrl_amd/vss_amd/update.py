@@ -96,8 +96,13 @@ def sum_parts(jobs) -> None:
         chunk = jobs[q0:q0 + 32]
         cols = {k: [] for k in ("src", "dst", "parts", "pstride", "rows", "cols", "sld", "dld")}
         for parts, out in chunk:
-            p3 = parts.reshape(parts.shape[0], -1, parts.shape[-1]) if parts.dim() >= 2 else None
-            o2 = out.reshape(1, -1) if out.dim() == 1 else out
+            # views only: a reshape that had to copy would hand the launch below a temporary's address
+            try:
+                p3 = parts.view(parts.shape[0], -1, parts.shape[-1]) if parts.dim() >= 2 else None
+                o2 = out.view(1, -1) if out.dim() == 1 else out
+            except RuntimeError as e:
+                raise ValueError(f"sum_parts: parts {tuple(parts.shape)} / out {tuple(out.shape)} are not "
+                                 f"viewable in the launch's shape ({e})") from None
             if p3 is None or parts.dtype != torch.float32 or out.dtype != torch.float32 or o2.dim() != 2 \
                     or tuple(p3.shape[1:]) != tuple(o2.shape) or p3.stride(2) != 1 or o2.stride(1) != 1 \
                     or not parts.is_cuda or out.device != parts.device:

@@ -10,6 +10,8 @@ import pytest
 import torch
 
 import ppo_continuous_action_isaacgym as P
+from vss_amd import minibatch as MB
+from vss_amd.update import sum_parts
 from test_ppo import _args, _synthetic_batch, make_agent
 from vss_amd.loss import (N_ACT, adv_part_sum, minibatch_gather, minibatch_gather_parts, ppo_loss, ppo_loss_direct,
                           ppo_loss_fused_finish, randperm)
@@ -48,6 +50,8 @@ def test_fused_loss_and_randperm_refuse_cpu_inputs_cpu():
                                   torch.zeros(1, 2), torch.zeros(2), gvb)
     with pytest.raises(ValueError):
         randperm(10, torch.zeros(1, dtype=torch.int64))
+    with pytest.raises(ValueError):  # key bits outside [1, 32]
+        randperm(10, torch.zeros(1, dtype=torch.int64), key_bits=33)
 
 
 def test_direct_minibatch_not_for_cpu_or_amp():
@@ -104,7 +108,7 @@ def test_output_backward_direct_matches_padded_pass_gpu(k_out):
     defer = []
     gz1, db1, dw1 = output_backward_direct(go, w, y, defer=defer)
     assert len(defer) == 2 and all(p.shape[0] <= 256 for p, _ in defer)
-    P.sum_parts(defer)
+    sum_parts(defer)
     assert torch.equal(gz0, gz1)
     ref_db, ref_dw = (go.double() @ w.double() * (1 - y.double() ** 2)).sum(0), go.double().t() @ y.double()
     for got, want in ((db0, ref_db), (db1, ref_db), (dw0, ref_dw), (dw1, ref_dw)):
@@ -216,7 +220,7 @@ def test_direct_minibatch_matches_autograd_path_gpu(n, nmb, act_dim, norm_adv, c
     against the autograd path on the same rows (index_select + normalize_advantages + minibatch_losses +
     zeroed_backward): every parameter's gradient within 2e-5 of its largest entry, the statistics within
     fp32 rounding; every gradient view written (the flat buffer starts as NaN)."""
-    monkeypatch.setattr(P, "FUSED_LOSS", fused)  # the loss in the last hidden layers' launches, or apart
+    monkeypatch.setattr(MB, "FUSED_LOSS", fused)  # the loss in the last hidden layers' launches, or apart
     args = _args(norm_adv=norm_adv, clip_vloss=clip_vloss, num_minibatches=nmb)
     g = torch.Generator().manual_seed(11)
     obs, _, logp, adv, ret, val = [t.cuda() for t in _synthetic_batch(5, n)]
@@ -265,15 +269,18 @@ def test_randperm_is_a_seeded_permutation_gpu(n):
 
 
 @pytest.mark.gpu
-def test_randperm_is_uniform_gpu():
+@pytest.mark.parametrize("key_bits", [32, 2, 1])
+def test_randperm_is_uniform_gpu(key_bits):
     """Uniformity of vss_randperm over seeds: for n = 8, 10,000 seeds, every (element, position) count
-    within 5 sigma of 1,250, and the fixed-point count's mean near 1 (a uniform permutation's)."""
+    within 5 sigma of 1,250, and the fixed-point count's mean near 1 (a uniform permutation's).  With 2 or 1
+    random key bits per index (4 or 2 key values for 8 indices) nearly every key is tied, so the result is
+    uniform only if the sort's tied runs are shuffled: a stable sort alone would keep them in index order."""
     n, draws = 8, 10000
-    seeds = torch.randint(-2 ** 62, 2 ** 62, (draws,), generator=torch.Generator().manual_seed(5))
+    seeds = torch.randint(-2 ** 62, 2 ** 62, (draws,), generator=torch.Generator().manual_seed(5 + key_bits))
     counts = torch.zeros(n, n, dtype=torch.int64)
     fixed = 0
     for s in seeds.tolist():
-        p = randperm(n, torch.tensor([s], dtype=torch.int64, device="cuda")).cpu()
+        p = randperm(n, torch.tensor([s], dtype=torch.int64, device="cuda"), key_bits=key_bits).cpu()
         counts[torch.arange(n), p] += 1
         fixed += int((p == torch.arange(n)).sum())
     expect = draws / n
@@ -282,13 +289,41 @@ def test_randperm_is_uniform_gpu():
     assert abs(fixed / draws - 1.0) < 0.05
 
 
+def _splitmix64(z):
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+@pytest.mark.gpu
+def test_randperm_ties_are_shuffled_at_batch_size_gpu():
+    """At the SA batch (8,388,608 indices, 32 random bits each) ~n^2 / 2^33 = 8,192 adjacent pairs of the
+    permutation carry tied random bits.  Recomputing every index's bits on the host (splitmix64 of seed and
+    index, as csrc/vss_loss.hip) from the permutation: the bits are sorted (non-decreasing), about the expected
+    number of tied pairs occur, and within tied pairs the lower index comes first half the time (a stable sort
+    alone: every time), within 5 sigma."""
+    n, seed = 8388608, 0x1234_5678_9ABC_DEF
+    p = randperm(n, torch.tensor([seed], dtype=torch.int64, device="cuda")).cpu().numpy()
+    assert np.array_equal(np.sort(p), np.arange(n))
+    with np.errstate(over="ignore"):
+        i = np.arange(n, dtype=np.uint64)
+        r = _splitmix64(np.uint64(seed) + (i + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(32)
+    keys = r[p]
+    assert bool(np.all(keys[1:] >= keys[:-1]))
+    tied = np.nonzero(keys[1:] == keys[:-1])[0]
+    expect = n * (n - 1) / 2 / 2 ** 32
+    assert abs(len(tied) - expect) < 5 * expect ** 0.5, (len(tied), expect)
+    ascending = float(np.mean(p[tied] < p[tied + 1]))
+    assert abs(ascending - 0.5) < 5 * (0.25 / len(tied)) ** 0.5, ascending
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("hip", [True, False])
 def test_epoch_permutations_gpu(hip, monkeypatch):
     """EpochPermutations on the GPU (side stream, drawn one epoch ahead): every epoch a permutation of the
     batch, the same sequence for the same generator seed; with VSS_RANDPERM=torch exactly torch.randperm's
     sequence from that generator."""
-    monkeypatch.setattr(P, "RANDPERM_HIP", hip)
+    monkeypatch.setattr(MB, "RANDPERM_HIP", hip)
     batch, epochs = 100000, 4
 
     def draw(seed):

@@ -12,6 +12,8 @@ import torch
 import torch.multiprocessing as mp
 
 import ppo_continuous_action_isaacgym as P
+from vss_amd import flat as F, minibatch as MB
+from vss_amd.writers import CsvWriter
 from envs._gym import Box
 
 Env = namedtuple("Env", ["single_observation_space", "single_action_space"])
@@ -107,7 +109,7 @@ def test_zeroed_backward_writes_the_autograd_gradients_gpu(rows, act_dim):
     flat.zeroed_backward(losses())
     for (name, p), w in zip(agent.named_parameters(), want):
         assert torch.equal(p.grad, w), name
-    assert not P._DIRECT_GRADS[0]
+    assert not F.DIRECT_GRADS[0]
 
 
 def _args(**kw):
@@ -236,7 +238,7 @@ def test_minibatch_graph_update_equals_eager_gpu(n, nmb, epochs, updates, norm_a
 
 def test_graph_check_schedule_is_geometric():
     """The captured minibatch is re-checked against eager at replays 12, 48, 192, ... (not once)."""
-    due = [r for r in range(1, 4000) if P.graph_check_due(r)]
+    due = [r for r in range(1, 4000) if MB.graph_check_due(r)]
     assert due == [12, 48, 192, 768, 3072]
 
 
@@ -244,7 +246,7 @@ def test_no_capture_when_packet_capture_is_on(monkeypatch):
     """A runtime started with graph packet capture on (switch unset or not "0") gets no captured
     minibatch: make_minibatch_graph warns once and returns None, so the update runs eagerly."""
     args = _args(norm_adv=True, clip_vloss=False, num_minibatches=4, update_epochs=1)
-    monkeypatch.setattr(P, "_WARNED_PACKET_CAPTURE", [False])
+    monkeypatch.setattr(MB, "_WARNED_PACKET_CAPTURE", [False])
     for value in (None, "1"):
         if value is None:
             monkeypatch.delenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE", raising=False)
@@ -254,6 +256,55 @@ def test_no_capture_when_packet_capture_is_on(monkeypatch):
             warnings.simplefilter("always")
             assert P.make_minibatch_graph(None, None, args, 1024, (52,), (2,), "cuda") is None
         assert len(w) == (1 if value is None else 0)  # once per process
+
+
+def test_capture_gate_uses_the_value_seen_before_gpu_init(monkeypatch):
+    """The capture gate asks what the runtime started with, not only what the environment says now: the
+    switch as vss_amd.minibatch last saw it while the GPU was uninitialised, else the process's startup
+    environment; a switch set to "0" only after the GPU initialised does not open the gate."""
+    monkeypatch.setenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+    monkeypatch.setattr(MB, "_SEEN_BEFORE_INIT", {"value": "0", "seen": True})
+    assert MB.packet_capture_off_at_init()
+    monkeypatch.setattr(MB, "_SEEN_BEFORE_INIT", {"value": None, "seen": True})  # unset when the runtime started
+    assert not MB.packet_capture_off_at_init()
+    monkeypatch.setattr(MB, "_SEEN_BEFORE_INIT", {"value": None, "seen": False})  # never seen before init
+    monkeypatch.setattr(MB, "_startup_environment_value", lambda: None)
+    assert not MB.packet_capture_off_at_init()
+    monkeypatch.setattr(MB, "_startup_environment_value", lambda: "0")
+    assert MB.packet_capture_off_at_init()
+    monkeypatch.setenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "1")  # changed since: not off now either
+    assert not MB.packet_capture_off_at_init()
+    # on a host whose GPU is not initialised, disable_graph_packet_capture records what it set
+    monkeypatch.delenv("DEBUG_CLR_GRAPH_PACKET_CAPTURE")
+    monkeypatch.setattr(MB.torch.cuda, "is_initialized", lambda: False)
+    monkeypatch.setattr(MB, "_SEEN_BEFORE_INIT", {"value": None, "seen": False})
+    assert MB.disable_graph_packet_capture() and MB.packet_capture_off_at_init()
+
+
+def test_flat_adam_clip_semantics_cpu():
+    """FlatAdam's clip request follows clip_grad_norm_: max_norm must be >= 0 (0 clips the gradients to zero,
+    as torch's does); without a request no clip is applied (the kernel's negative sentinel)."""
+    assert F.FlatAdam.NO_CLIP < 0
+    adam = F.FlatAdam.__new__(F.FlatAdam)
+    with pytest.raises(ValueError):
+        adam.defer_clip(-1.0)
+    with pytest.raises(ValueError):
+        adam.defer_clip(float("nan"))
+
+
+@pytest.mark.gpu
+def test_flat_adam_zero_max_norm_zeroes_like_clip_grad_norm_gpu():
+    """max_norm = 0: clip_grad_norm_ scales every gradient by 0 / (norm + 1e-6) = 0, so Adam's first step
+    moves nothing; FlatAdam does the same (round 5's kernel treated 0 as 'no clip')."""
+    agent = make_agent(2).cuda()
+    flat = P.FlatGrads(agent, flat_params=True)
+    opt = P.FlatAdam(flat, lr=1e-3, eps=1e-5)
+    before = flat.flat_p.clone()
+    flat.flat.copy_(torch.randn(flat.flat.numel(), device="cuda"))
+    norm = flat.clip_norm_(0.0)
+    opt.step()
+    assert float(flat.flat.abs().max()) == 0.0 and torch.equal(flat.flat_p, before)
+    assert float(norm) > 0
 
 
 @pytest.mark.gpu
@@ -267,7 +318,7 @@ def test_minibatch_graph_self_check_gpu(corrupt):
     # 4 minibatches x 13 epochs = 52 minibatches: replays 1 .. 51 cover the checks at 12 and 48
     args = _args(norm_adv=True, clip_vloss=False, num_minibatches=4, update_epochs=13)
     n = 32768
-    bad_replay = {None: None, "first": P.GRAPH_CHECK_REPLAY, "later": P.GRAPH_CHECK_REPLAY * P.GRAPH_CHECK_FACTOR}[corrupt]
+    bad_replay = {None: None, "first": MB.GRAPH_CHECK_REPLAY, "later": MB.GRAPH_CHECK_REPLAY * MB.GRAPH_CHECK_FACTOR}[corrupt]
     obs, act, logp, adv, ret, val = [t.cuda() for t in _synthetic_batch(5, n)]
     res = []
     for use_graph in (False, True):
@@ -326,7 +377,7 @@ def test_padded_minibatch_update_matches_unpadded_gpu(n, monkeypatch):
     data = [t.cuda() for t in _synthetic_batch(9, n)]
     res = []
     for pad in (256, 1):
-        monkeypatch.setattr(P, "MLP_ROW_PAD", pad)
+        monkeypatch.setattr(MB, "MLP_ROW_PAD", pad)
         agent = make_agent(2).cuda()
         flat = P.FlatGrads(agent)
         opt = torch.optim.Adam(agent.parameters(), lr=1e-3, eps=1e-5)
@@ -339,7 +390,7 @@ def test_padded_minibatch_update_matches_unpadded_gpu(n, monkeypatch):
 def test_minibatch_graph_refuses_other_shapes():
     """run() checks the minibatch against the captured static buffers before touching them (a CPU
     stand-in object: no capture happens before the check)."""
-    g = P.MinibatchGraph.__new__(P.MinibatchGraph)
+    g = MB.MinibatchGraph.__new__(MB.MinibatchGraph)
     g.obs, g.act, g.logp = torch.zeros(256, 52), torch.zeros(256, 2), torch.zeros(200)
     with pytest.raises(ValueError, match="does not match"):
         g.run(torch.arange(100), torch.arange(256), torch.zeros(10, 52), torch.zeros(10, 2), None, None, None, None)
@@ -456,7 +507,7 @@ def test_fused_rollout_next_values_equal_reference_definition(tmp_path, form, E)
     from envs.vss import default_cfg
     from envs.wrappers import SingleAgent
     from envs.vss import VSS
-    from vss_amd.policy import FusedPolicy
+    from vss_amd.policy import FusedPolicy, TerminalValues
     cfg = default_cfg(E)
     cfg["env"]["maxEpisodeLength"] = 8
     cfg["env"]["seed"] = 5
@@ -469,7 +520,7 @@ def test_fused_rollout_next_values_equal_reference_definition(tmp_path, form, E)
     term = torch.zeros((T, E), device="cuda")
     full = torch.zeros((T, E), device="cuda")
     dones = torch.zeros((T, E), device="cuda")
-    tv = P.TerminalValues(T, E, (52,), "cuda")
+    tv = TerminalValues(T, E, (52,), "cuda")
     o = W.reset()["obs"]
     for t in range(T):
         a, lp, _, v = fused.get_action_and_value(o)
@@ -492,7 +543,7 @@ def test_fused_rollout_next_values_equal_reference_definition(tmp_path, form, E)
 
 
 def test_csv_writer_fallback(tmp_path):
-    w = P._CsvWriter(os.path.join(tmp_path, "run", "scalars.csv"))
+    w = CsvWriter(os.path.join(tmp_path, "run", "scalars.csv"))
     w.add_scalar("losses/value_loss", 0.5, 10)
     w.add_scalar("rws/episodic_return", torch.tensor(-1.25), 20)
     w.close()

@@ -7,6 +7,7 @@ import pytest
 import torch
 
 import ppo_continuous_action_isaacgym as P
+from vss_amd import mlp as M
 from vss_amd import _native as N
 from vss_amd.update import linear_tanh, linear_tanh_backward, output_backward, tanh_grad_bias
 
@@ -220,7 +221,7 @@ def test_update_gradients_through_hip_match_autograd_gpu(rows, gemm, act_dim, mo
     ones); its gradients (fused HIP GEMM epilogues, split weight gradients) equal autograd's up to fp32
     summation order.  act_dim 6 (the CMA actor: 6 output columns padded to k_pad = 8 in
     vss_output_backward) as well as 2 (SA/DMA: k_pad = 4; the 1-column critic pads to 4 in both)."""
-    monkeypatch.setattr(P, "UPDATE_GEMM", gemm)
+    monkeypatch.setattr(M, "UPDATE_GEMM", gemm)
     agent = make_agent(act_dim).cuda()
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.randn(rows, 52, device="cuda", generator=g)
@@ -310,7 +311,7 @@ def test_update_gradients_on_rollout_data_at_fp32_error_gpu():
         return [t.double() for t in torch.autograd.grad(loss, list(ag.parameters()))]
 
     def product(ag, x_, a_, lp_, ad_, r_, v_):  # the update's path: _TanhMLP (x6) + vss_ppo_loss
-        return ppo_loss(P._mlp_forward(ag.actor_mean, x_), ag.actor_logstd, P._mlp_forward(ag.critic, x_), a_, lp_, ad_,
+        return ppo_loss(M.mlp_forward(ag.actor_mean, x_), ag.actor_logstd, M.mlp_forward(ag.critic, x_), a_, lp_, ad_,
                         r_, v_, *coef)
 
     def plain(ag, x_, a_, lp_, ad_, r_, v_):  # torch autograd of the reference's expressions

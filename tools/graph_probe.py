@@ -11,6 +11,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 import torch  # noqa: E402
 
 import ppo_continuous_action_isaacgym as P  # noqa: E402
+from vss_amd import minibatch as MBM, mlp as MLP  # noqa: E402
 from envs._gym import Box  # noqa: E402
 
 
@@ -24,15 +25,15 @@ def agent():
 
 def main():
     if os.environ.get("SYNC_REPLAY"):  # wait for every replay before the eager work after it
-        orig = P.MinibatchGraph.run
+        orig = MBM.MinibatchGraph.run
 
         def run(self, *a):
             st = orig(self, *a)
             torch.cuda.synchronize()
             return st
-        P.MinibatchGraph.run = run
+        MBM.MinibatchGraph.run = run
     if os.environ.get("NOSPLITK"):
-        P.SPLITK_MIN_ROWS = 1 << 62  # the first layer's weight gradient as one mm instead of bmm + sum
+        MLP.SPLITK_MIN_ROWS = 1 << 62  # the first layer's weight gradient as one mm instead of bmm + sum
     for mb in [int(v) for v in os.environ.get("MBS", "16384,32768,65536,262144,2097152").split(",")]:
         n = int(os.environ.get("NMB", 2)) * mb
         args = P.parse_args([])

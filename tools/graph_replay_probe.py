@@ -32,17 +32,18 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import ppo_continuous_action_isaacgym as P  # noqa: E402
+from vss_amd import minibatch as MBM, mlp as MLP  # noqa: E402
 from envs._gym import Box  # noqa: E402
 from vss_amd import update as U  # noqa: E402
 
 if PATH == "torch":
-    P._mlp_forward = lambda seq, x: seq(x)
+    MLP.mlp_forward = lambda seq, x: seq(x)
 # LOSS=torch: the minibatch loss as the reference's torch expressions and their autograd (~100 small
 # kernels; what the update ran before vss_ppo_loss) instead of the fused HIP loss
 LOSS = os.environ.get("LOSS", "fused")
 if LOSS == "torch":
     from vss_amd.loss import reference_loss
-    P.ppo_loss = reference_loss
+    MBM.ppo_loss = reference_loss
 
 R = int(os.environ.get("REPLAYS", 16))
 MB = int(os.environ.get("MB", 2097152))
@@ -124,7 +125,7 @@ def stage_mlp():
     def body():
         for p in params:
             p.grad = None
-        out = P._mlp_forward(a.actor_mean, x)
+        out = MLP.mlp_forward(a.actor_mean, x)
         grads = torch.autograd.grad(out, params, gout)
         return [out.detach()] + [t.detach() for t in grads]
     return replay_check(f"mlp actor fwd+bwd ({PATH})", body, lambda r: r)
@@ -136,7 +137,7 @@ def stage_minibatch():
     args = P.parse_args([])
     g = torch.Generator(device="cuda").manual_seed(3)
     pad = P.padding_rows(MB, "cuda")
-    mbg = P.MinibatchGraph(a, flat, args, MB, (52,), (2,), "cuda")
+    mbg = MBM.MinibatchGraph(a, flat, args, MB, (52,), (2,), "cuda")
     mbg.obs.copy_(torch.randn(MB + pad, 52, device="cuda", generator=g))
     mbg.act.copy_(torch.randn(MB + pad, 2, device="cuda", generator=g) * 0.5)
     for t in (mbg.logp, mbg.adv, mbg.ret, mbg.val):
@@ -161,7 +162,7 @@ def stage_ppo():
         a = agent()
         flat = P.FlatGrads(a)
         opt = torch.optim.Adam(a.parameters(), lr=1e-3, eps=1e-5)
-        graph = P.MinibatchGraph(a, flat, args, MB, (52,), (2,), "cuda") if use_graph else None
+        graph = MBM.MinibatchGraph(a, flat, args, MB, (52,), (2,), "cuda") if use_graph else None
         st = P.ppo_update(a, opt, flat, args, obs, logp, act, adv, ret, val,
                           gen=torch.Generator(device="cuda").manual_seed(7), graph=graph)
         out.append((torch.cat([p.detach().reshape(-1) for p in a.parameters()]), st))

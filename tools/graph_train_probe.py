@@ -9,8 +9,9 @@ sys.path.insert(0, os.path.join(REPO, "rsoccer-isaac-cleanrl_amd"))
 import torch  # noqa: E402
 
 import ppo_continuous_action_isaacgym as P  # noqa: E402
+from vss_amd import minibatch as MBM, mlp as MLP  # noqa: E402
 
-_orig = P.MinibatchGraph.run
+_orig = MBM.MinibatchGraph.run
 _count = [0]
 
 
@@ -29,7 +30,7 @@ def run(self, *a):
     return st
 
 
-P.MinibatchGraph.run = run
+MBM.MinibatchGraph.run = run
 args = P.parse_args(["--env-id", "sa", "--num-envs", os.environ.get("NUM_ENVS", "65536"), "--num-updates",
                      os.environ.get("UPDATES", "1"), "--log", "false", "--seed", "1", "--save-path", "/tmp/runs"])
 _, hist = P.train(args)

@@ -1,0 +1,363 @@
+// Profiling-only: the ceiling of the x6 backward 512 <- 256 (csrc/vss_gemm_x6.hip gemm_x6_kernel<EPI_DTANH,
+// ST_DMA, ST_ROW, CfgB>: gz = (g W) (1 - y^2) at 2,097,152 rows, K = 256, 512 features), built up from the
+// matrix-core loop one piece of the product kernel's work at a time (round-5 VERDICT Next 3).  Every stage
+// keeps the product's geometry -- 256-feature x 128-row blocks of 8 waves (4 x 2, 64 x 64 each), one block
+// per CU persistent over the 32,768 items (2 i tiles x 16,384 row bands) with the XCD-aware slot map, K tiles
+// of 32 in two LDS buffers with a barrier after each, the six bf16 products per K step -- and adds:
+//
+//   0 lds    the fragments read from the LDS buffers, MFMAs, barriers (the operand images never change)
+//   1 +q     the activation tile's global loads (2 x 16 B per thread per K tile from the (rows, 256) g), issued
+//            where the product issues them; consumed by a register sink, not written
+//   2 +split the loaded tile split into three bf16 planes and written into the other buffer (the product's
+//            register staging)
+//   3 +dma   the weight tile's three planes copied global -> LDS per K tile by global_load_lds (6 x 1 KB per
+//            wave), from the 768-KB plane image (L2-resident), as the product
+//   4 +store the epilogue's nontemporal stores of the item's 128 x 256 outputs and the column sums
+//   5 +y     the epilogue's y loads (one row group prefetched at the last K-tile pair, the rest at the
+//            epilogue's start) and the tanh derivative: the product's work
+//
+// For each stage: wall time per launch (HIP events over >= 2 s of back-to-back launches, after 1 s of
+// warm-up), fp32-equivalent TF (2 rows 512 256 / time), the in-kernel clock (s_memtime / s_memrealtime x
+// 100 MHz around each wave's item loop, median over waves; MI355X_MICROARCH.md DVFS item 6) and the matrix
+// pipes' busy fraction implied by them (bf16 FLOP / (clock x 1024 FLOP per SIMD-cycle x 1024 SIMDs)).
+//
+//   hipcc -O3 --offload-arch=gfx950 -o tools/_build/x6_buildup tools/x6_buildup.hip
+//   tools/_build/x6_buildup [stage ...]    -> one JSON line per stage
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <vector>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BI = 256, BJ = 128, WI = 4, WJ = 2, THREADS = 512, TI = 4, TJ = 4, WTI = 64, WTJ = 64;
+constexpr int KT = 32, KTILES = 8, NI = 2;             // K = 256, n = 512
+constexpr int GS_P = BI * 16, PS_P = 4 * GS_P, IMG_P = 3 * PS_P;  // 48 KB
+constexpr int GS_Q = BJ * 16, PS_Q = 4 * GS_Q, IMG_Q = 3 * PS_Q;  // 24 KB
+constexpr int BUF = IMG_P + IMG_Q, LDS = 2 * BUF;                 // 144 KB
+constexpr int NQ = IMG_P / (THREADS / 64) / 1024;                 // 6 DMA slices per wave per K tile
+constexpr int64_t ROWS = 2097152, LDQ = 256, LDO = 512;
+constexpr int ITEMS = NI * (int)(ROWS / BJ);
+constexpr int GRID = 256;
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  const bf16x2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+__device__ __forceinline__ void split8(const float (&v)[8], u32x4& hi, u32x4& mid, u32x4& lo) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float a = v[2 * p], b = v[2 * p + 1];
+    const uint32_t h = pk_bf16(a, b);
+    const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xFFFF0000u);
+    const uint32_t m = pk_bf16(ra, rb);
+    const float sa = ra - __uint_as_float(m << 16), sb = rb - __uint_as_float(m & 0xFFFF0000u);
+    hi[p] = h;
+    mid[p] = m;
+    lo[p] = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
+  }
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f32<0xB1>(v);
+  v += dpp_f32<0x4E>(v);
+  v += dpp_f32<0x141>(v);
+  v += dpp_f32<0x140>(v);
+  return v;
+}
+
+template <int S>
+__global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __restrict__ q, const char* __restrict__ pimg,
+                                                             const float* __restrict__ y, float* __restrict__ out,
+                                                             float* __restrict__ partial, float* __restrict__ sinkbuf,
+                                                             uint64_t* __restrict__ stamps) {
+  __shared__ __attribute__((aligned(16))) char lds[LDS + WJ * BI * 4];
+  float* cs_lds = reinterpret_cast<float*>(lds + LDS);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wi = wv / WJ, wj = wv % WJ;
+  const int G = gridDim.x;
+  const int slot = (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8);
+  const int it0 = slot % NI;
+  for (int i = tid; i < WJ * BI; i += THREADS) cs_lds[i] = 0.f;
+  // the operand images the stages that do not (re)write them read: tile 0 of the weight image in both
+  // buffers' P part, and its first 24 KB as the Q part (random bf16 planes either way)
+  for (int i = tid; i < LDS / 16; i += THREADS) {
+    const int off = (i * 16) % BUF, src = off < IMG_P ? off : off - IMG_P;
+    *reinterpret_cast<u32x4*>(lds + i * 16) = *reinterpret_cast<const u32x4*>(pimg + it0 * KTILES * IMG_P + src);
+  }
+  __syncthreads();
+
+  uint32_t sink = 0;
+  float fsink = 0.f;
+  int f_item = slot, f_kt = 0;
+  auto gload = [&](u32x4 (&s)[2]) {
+    if constexpr (S >= 1) {
+      const int jt = f_item / NI;
+      const int g = (tid >> 3) & 3, row = (tid & 7) | ((tid >> 5) << 3);
+      const float* src = q + ((int64_t)jt * BJ + row) * LDQ + f_kt * KT + 8 * g;
+      s[0] = *reinterpret_cast<const u32x4*>(src);
+      s[1] = *reinterpret_cast<const u32x4*>(src + 4);
+      if (++f_kt >= KTILES) {
+        if (f_item + G < ITEMS) {
+          f_kt = 0;
+          f_item += G;
+        } else {
+          f_kt = KTILES - 1;
+        }
+      }
+    }
+  };
+  auto swrite = [&](const u32x4 (&s)[2], int buf) {
+    if constexpr (S >= 2) {
+      const int g = (tid >> 3) & 3, row = (tid & 7) | ((tid >> 5) << 3);
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = __uint_as_float(s[e >> 2][e & 3]);
+      u32x4 hi, mid, lo;
+      split8(v, hi, mid, lo);
+      char* d = lds + buf * BUF + IMG_P + g * GS_Q + row * 16;
+      *reinterpret_cast<u32x4*>(d) = hi;
+      *reinterpret_cast<u32x4*>(d + PS_Q) = mid;
+      *reinterpret_cast<u32x4*>(d + 2 * PS_Q) = lo;
+    } else if constexpr (S >= 1) {
+      sink ^= s[0][0] ^ s[0][1] ^ s[0][2] ^ s[0][3] ^ s[1][0] ^ s[1][1] ^ s[1][2] ^ s[1][3];
+    }
+  };
+  auto dma_p = [&](int kt, int buf) {
+    if constexpr (S >= 3) {
+      const int64_t off = ((int64_t)it0 * KTILES + kt) * IMG_P;
+#pragma unroll
+      for (int qq = 0; qq < NQ; ++qq) {
+        const int sl = (wv * NQ + qq) * 1024;
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(pimg + off + sl + lane * 16),
+                                         (__attribute__((address_space(3))) void*)(lds + buf * BUF + sl), 16, 0, 0);
+      }
+    }
+  };
+  f32x4 acc[TI][TJ];
+  const int fr = lane & 15, fg = lane >> 4;
+  auto mfma_tile = [&](int buf, auto&& between) {
+    const char* pb = lds + buf * BUF + fg * GS_P + (wi * WTI + fr) * 16;
+    const char* qb = lds + buf * BUF + IMG_P + fg * GS_Q + (wj * WTJ + fr) * 16;
+    u32x4 pf[3][TI], qf[3][TJ];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int i = 0; i < TI; ++i) pf[pl][i] = *reinterpret_cast<const u32x4*>(pb + pl * PS_P + i * 256);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) qf[pl][j] = *reinterpret_cast<const u32x4*>(qb + pl * PS_Q + j * 256);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    between();
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int PP[6] = {2, 0, 1, 1, 0, 0};
+    constexpr int QP[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+    for (int x = 0; x < 6; ++x)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pf[PP[x]][i]),
+                                                              __builtin_bit_cast(bf16x8, qf[QP[x]][j]), acc[i][j], 0, 0, 0);
+  };
+
+  u32x4 r0[2] = {}, r1[2] = {};
+  gload(r0);
+  dma_p(0, 0);
+  swrite(r0, 0);
+  gload(r1);
+  gload(r0);
+  __syncthreads();
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), c0 = __builtin_amdgcn_s_memrealtime();
+  for (int w = slot; w < ITEMS; w += G) {
+    const bool has_next = w + G < ITEMS;
+    const int it = w % NI, jt = w / NI;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    f32x4 ypre[TI];
+    const int64_t jb = (int64_t)jt * BJ + wj * WTJ;
+    const int ib = it * BI + wi * WTI;
+    for (int kt = 0; kt < KTILES; kt += 2) {
+      if constexpr (S >= 5) {
+        if (kt + 2 >= KTILES) {
+#pragma unroll
+          for (int i = 0; i < TI; ++i) ypre[i] = *reinterpret_cast<const f32x4*>(y + (jb + fr) * LDO + ib + 16 * i + 4 * fg);
+        }
+      }
+      mfma_tile(0, [&] { dma_p(kt + 1, 1); });
+      swrite(r1, 1);
+      __syncthreads();
+      gload(r1);
+      mfma_tile(1, [&] {
+        if (kt + 2 < KTILES) dma_p(kt + 2, 0);
+        else if (has_next) dma_p(0, 0);
+      });
+      swrite(r0, 0);
+      __syncthreads();
+      gload(r0);
+    }
+    if constexpr (S >= 4) {
+      float cs[TI][4];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) cs[i][0] = cs[i][1] = cs[i][2] = cs[i][3] = 0.f;
+      f32x4 yrest[TJ][TI];
+      if constexpr (S >= 5) {
+#pragma unroll
+        for (int j = 1; j < TJ; ++j)
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+            yrest[j][i] = *reinterpret_cast<const f32x4*>(y + (jb + 16 * j + fr) * LDO + ib + 16 * i + 4 * fg);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int64_t jg = jb + 16 * j + fr;
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          f32x4 v = acc[i][j];
+          if constexpr (S >= 5) {
+            const f32x4 yv = j == 0 ? ypre[i] : yrest[j][i];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = v[r] * fmaf(-yv[r], yv[r], 1.0f);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cs[i][r] += v[r];
+          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + jg * LDO + ib + 16 * i + 4 * fg));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t = row16_sum(cs[i][r]);
+          if (fr == 0) cs_lds[wj * BI + wi * WTI + 16 * i + 4 * fg + r] += t;
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) fsink += acc[i][j][0] + acc[i][j][3];  // keeps the MFMAs live
+    }
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), c1 = __builtin_amdgcn_s_memrealtime();
+  __syncthreads();
+  if constexpr (S >= 4) {
+    for (int f = tid; f < BI; f += THREADS) partial[(int64_t)slot * BI + f] = cs_lds[f] + cs_lds[BI + f];
+  }
+  sinkbuf[blockIdx.x * THREADS + tid] = fsink + (float)(sink & 1);
+  if (lane == 0) {
+    const int wg = blockIdx.x * (THREADS / 64) + wv;
+    stamps[2 * wg] = t1 - t0;
+    stamps[2 * wg + 1] = c1 - c0;
+  }
+}
+
+#define CK(x)                                                 \
+  do {                                                        \
+    hipError_t e_ = (x);                                      \
+    if (e_ != hipSuccess) {                                   \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); \
+      exit(1);                                                \
+    }                                                         \
+  } while (0)
+
+struct Bufs {
+  float *q, *y, *out, *partial, *sink;
+  char* pimg;
+  uint64_t* stamps;
+};
+
+template <int S>
+static void run(const char* name, const Bufs& b) {
+  auto launch = [&] {
+    hipLaunchKernelGGL(buildup_kernel<S>, dim3(GRID), dim3(THREADS), 0, 0, b.q, b.pimg, b.y, b.out, b.partial, b.sink,
+                       b.stamps);
+  };
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  float ms = 0.f;
+  CK(hipEventRecord(e0, 0));
+  while (ms < 1000.f) {  // warm-up: the clock settles under load
+    for (int i = 0; i < 10; ++i) launch();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+  }
+  CK(hipGetLastError());
+  int launches = 0;
+  ms = 0.f;
+  CK(hipEventRecord(e0, 0));
+  while (ms < 2000.f) {
+    for (int i = 0; i < 10; ++i) launch();
+    launches += 10;
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+  }
+  const int waves = GRID * THREADS / 64;
+  std::vector<uint64_t> st(2 * waves);
+  CK(hipMemcpy(st.data(), b.stamps, st.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<double> clk(waves);
+  for (int w = 0; w < waves; ++w) clk[w] = (double)st[2 * w] / (double)st[2 * w + 1] * 100e6;
+  std::sort(clk.begin(), clk.end());
+  const double per = ms / launches;
+  const double tf = 2.0 * ROWS * LDO * LDQ / (per * 1e-3) / 1e12;     // fp32-equivalent
+  const double ghz = clk[waves / 2] / 1e9;
+  const double busy = 6.0 * tf * 1e12 / (ghz * 1e9 * 1024.0 * 1024.0);  // 1024 SIMDs x 1024 bf16 FLOP per cycle
+  printf("{\"stage\": \"%s\", \"launches\": %d, \"ms_per_launch\": %.4f, \"x6_tflops\": %.1f, \"frac_of_x6_peak\": %.4f, "
+         "\"clock_ghz_median\": %.3f, \"clock_min\": %.3f, \"clock_max\": %.3f, \"mfma_busy_implied\": %.3f}\n",
+         name, launches, per, tf, tf / (2500.0 / 6), ghz, clk[0] / 1e9, clk[waves - 1] / 1e9, busy);
+  fflush(stdout);
+}
+
+__global__ void fill_kernel(uint32_t* p, int64_t n, uint32_t seed, int kind) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+    x ^= x >> 15;
+    x *= 2246822519u;
+    x ^= x >> 13;
+    const float u = (float)(x >> 8) * (1.0f / 16777216.0f);  // [0, 1)
+    if (kind == 0) p[i] = __float_as_uint(u * 2.f - 1.f);          // activations / y in (-1, 1)
+    else p[i] = (0x3F00u | (x & 0x80FFu)) | ((0x3F00u | ((x >> 16) & 0x80FFu)) << 16);  // random bf16 pairs
+  }
+}
+
+int main(int argc, char** argv) {
+  Bufs b;
+  CK(hipMalloc(&b.q, ROWS * LDQ * 4));
+  CK(hipMalloc(&b.y, ROWS * LDO * 4));
+  CK(hipMalloc(&b.out, ROWS * LDO * 4));
+  CK(hipMalloc(&b.partial, (size_t)GRID * BI * 4));
+  CK(hipMalloc(&b.sink, (size_t)GRID * THREADS * 4));
+  CK(hipMalloc(&b.pimg, (size_t)NI * KTILES * IMG_P));
+  CK(hipMalloc(&b.stamps, (size_t)GRID * THREADS / 64 * 16));
+  hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint32_t*)b.q, ROWS * LDQ, 1u, 0);
+  hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint32_t*)b.y, ROWS * LDO, 2u, 0);
+  hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, 0, (uint32_t*)b.pimg, (int64_t)NI * KTILES * IMG_P / 4, 3u, 1);
+  CK(hipDeviceSynchronize());
+  bool want[6] = {true, true, true, true, true, true};
+  if (argc > 1) {
+    for (int s = 0; s < 6; ++s) want[s] = false;
+    for (int a = 1; a < argc; ++a) want[atoi(argv[a]) % 6] = true;
+  }
+  if (want[0]) run<0>("0 lds", b);
+  if (want[1]) run<1>("1 +q", b);
+  if (want[2]) run<2>("2 +split", b);
+  if (want[3]) run<3>("3 +dma", b);
+  if (want[4]) run<4>("4 +store", b);
+  if (want[5]) run<5>("5 +y (product work)", b);
+  return 0;
+}

@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Profiling-only: the product's x6 backward 512 <- 256 (vss_linear_tanh_backward_bf16x6 at 2,097,152 rows) timed
+the way tools/x6_buildup.hip times its stages (1 s warm-up, then >= 2 s of back-to-back launches, HIP events), on
+random data, so the build-up's last stage and the product kernel can be compared on one box."""
+import os
+import sys
+import json
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "rsoccer-isaac-cleanrl_amd"))
+import torch  # noqa: E402
+
+from vss_amd import update as U  # noqa: E402
+
+rows, k_next, n = 2097152, 256, 512
+g = torch.Generator(device="cuda").manual_seed(1)
+gn = torch.rand(rows, k_next, device="cuda", generator=g) * 2 - 1
+w = (torch.rand(k_next, n, device="cuda", generator=g) * 2 - 1) / 16
+y = torch.rand(rows, n, device="cuda", generator=g) * 2 - 1
+out = torch.empty(rows, n, device="cuda")
+planes = U.weight_planes([(w, True)])[0]
+
+
+def launch():
+    U.linear_tanh_backward_x6(gn, w, y, out=out, planes=planes, defer=[])
+
+
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+for seconds, timed in ((1.0, False), (2.0, True)):
+    launches, ms = 0, 0.0
+    e0.record()
+    while ms < seconds * 1e3:
+        for _ in range(10):
+            launch()
+        launches += 10
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+per = ms / launches
+tf = 2.0 * rows * n * k_next / (per * 1e-3) / 1e12
+print(json.dumps({"stage": "product vss_linear_tanh_backward_bf16x6 512<-256", "launches": launches, "ms_per_launch": per,
+                  "x6_tflops": tf, "frac_of_x6_peak": tf / (2500.0 / 6),
+                  "note": "wall includes the defer=[] partial-sum path (no reduction launch) per call"}), flush=True)

@@ -361,6 +361,7 @@ def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
                                   "ranks); first_update_overhead_s = the first update's delta minus it (env reset, the "
                                   "minibatch graph capture, remaining first uses)"),
             "kernel_warmup_s": getattr(args, "kernel_warmup_s", 0.0),
+            "graph_prepare_s": getattr(args, "graph_prepare_s", 0.0),
             "kernel_warmup": ("BEFORE the train clock (ppo…:244), outside wallclock_to_1e8_steps_s: one 8-step update of "
                               "the same loop on a throwaway 16,384-env env and Agent copy (--kernel-warmup, "
                               "warmup_kernels), so the runtime's first-use code-object loading of the loop's kernels "
@@ -379,11 +380,21 @@ def ppo_dma_leg(n_fields: int, updates: int, dev, world: int = 1) -> dict:
     _, hist = P.train(args)
     last = hist[-1]
     red = dev if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu"
-    roll_s, upd_s = reduce_max([last["rollout_s"], last["update_s"]], red)
+    roll_s, upd_s, first_upd_s = reduce_max([last["rollout_s"], last["update_s"], hist[0]["update_s"]], red)
+    walls = reduce_max([h["wall_s"] for h in hist], red)
+    deltas = [walls[0]] + [b - a for a, b in zip(walls, walls[1:])]
+    steady = float(np.median(deltas[1:])) if len(deltas) > 1 else None
     rows = args.num_envs * world
     return {"env": "dma", "n_gpus": world, "fields_per_gpu": n_fields, "agent_rows": rows,
             "num_steps": args.num_steps, "batch": args.batch_size * world, "minibatch_rows": args.minibatch_size,
             "updates_run": len(hist), "rollout_s": roll_s, "update_s": upd_s,
+            "first_update_s": deltas[0], "steady_s_per_update": steady,
+            "kernel_warmup_s": getattr(args, "kernel_warmup_s", 0.0), "graph_prepare_s": getattr(args, "graph_prepare_s", 0.0),
+            "first_update_update_s": first_upd_s, "first_to_steady_update_ratio": first_upd_s / upd_s,
+            "first_update_note": ("first_update_s / steady_s_per_update: the train clock's first delta and the median of "
+                                  "the later ones (max over ranks); first_update_update_s: the first update's update phase "
+                                  "(it holds the eager first minibatch, the capture and the replay-12 self-check, all in "
+                                  "one memory pool) against the last one's update_s"),
             "rollout_agent_steps_per_s": rows * args.num_steps / roll_s,
             "train_agent_steps_per_s": rows * args.num_steps / (roll_s + upd_s),
             "mean_return_last": last["mean_return"], "v_loss_last": last["v_loss"], "entropy_last": last["entropy"]}

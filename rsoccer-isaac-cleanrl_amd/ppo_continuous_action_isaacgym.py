@@ -399,6 +399,12 @@ def train(args, on_update=None):
     # uses on a throwaway copy of the loop (warmup_kernels); args.kernel_warmup_s keeps the time it took
     args.kernel_warmup_s = warmup_kernels(args, train) if getattr(args, "kernel_warmup", False) and device.type == "cuda" \
         else 0.0
+    # and the update minibatch's device memory and graph capture (MinibatchGraph.prepare), on the empty storage
+    t_prep = time.perf_counter()
+    if graph is not None:
+        graph.prepare(obs.reshape((-1,) + obs_dim), actions.reshape((-1,) + act_dim), logprobs.reshape(-1),
+                      values.reshape(-1), values.reshape(-1), values.reshape(-1), world)
+    args.graph_prepare_s = time.perf_counter() - t_prep
     global_step = 0
     start_time = time.time()
     next_obs = envs.reset()

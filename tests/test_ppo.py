@@ -221,19 +221,24 @@ def test_minibatch_graph_update_equals_eager_gpu(n, nmb, epochs, updates, norm_a
     args = _args(norm_adv=norm_adv, clip_vloss=clip_vloss, num_minibatches=nmb, update_epochs=epochs)
     obs, act, logp, adv, ret, val = [t.cuda() for t in _synthetic_batch(5, n)]
     res = []
-    for use_graph in (False, True):
+    for mode in ("eager", "graph", "prepared"):
         agent = make_agent(2).cuda()
         flat = P.FlatGrads(agent)
         opt = torch.optim.Adam(agent.parameters(), lr=1e-3, eps=1e-5)
-        graph = P.make_minibatch_graph(agent, flat, args, n, (52,), (2,), "cuda") if use_graph else None
-        assert (graph is not None) == use_graph
+        graph = P.make_minibatch_graph(agent, flat, args, n, (52,), (2,), "cuda") if mode != "eager" else None
+        assert (graph is not None) == (mode != "eager")
+        if mode == "prepared":  # train()'s set-up before the clock: eager first minibatch + capture on empty rows
+            z = torch.zeros(n, device="cuda")
+            graph.prepare(torch.zeros_like(obs), torch.zeros_like(act), z, z, z, z)
+            assert graph.graph is not None and float(flat.flat.abs().sum()) == 0.0
         gen = torch.Generator(device="cuda").manual_seed(7)
         stats = [P.ppo_update(agent, opt, flat, args, obs, logp, act, adv, ret, val, gen=gen, graph=graph)
                  for _ in range(updates)]
         res.append((torch.cat([p.detach().reshape(-1) for p in agent.parameters()]), stats))
-    assert torch.equal(res[0][0], res[1][0])
-    for a, b in zip(res[0][1], res[1][1]):
-        assert {k: float(v) for k, v in a.items()} == {k: float(v) for k, v in b.items()}
+    for other in res[1:]:
+        assert torch.equal(res[0][0], other[0])
+        for a, b in zip(res[0][1], other[1]):
+            assert {k: float(v) for k, v in a.items()} == {k: float(v) for k, v in b.items()}
 
 
 def test_graph_check_schedule_is_geometric():

@@ -33,8 +33,7 @@ COEF = dict(clip_coef=0.2, ent_coef=0.005, vf_coef=4.0, clip_vloss=False)  # the
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.fixture(scope="module")
-def rollout_rows():
+def make_rollout_rows():
     """(agent, obs, act, logp_old, adv, ret, val): 2,097,152 rows of observations from 512 steps of the fused
     SA env at 4,096 fields under random actions, actions drawn from the Agent's policy, old log-probs within
     ~0.1 of the current ones (ratios around 1, some clipped), RAW advantages (mean 0.7, std 2.5: the
@@ -62,6 +61,11 @@ def rollout_rows():
     return agent, x, act.contiguous(), logp_old, adv, ret, val
 
 
+@pytest.fixture(scope="module")
+def rollout_rows():
+    return make_rollout_rows()
+
+
 _REF = {}
 
 
@@ -73,7 +77,7 @@ def _reference_grads(agent0, data, inds, dtype):
     a = (adv - adv.mean()) / (adv.std() + 1e-8)
     loss, _ = reference_loss(ag.actor_mean(x), ag.actor_logstd, ag.critic(x), act, lp, a, ret, val, **COEF)
     grads = [t.double() for t in torch.autograd.grad(loss, list(ag.parameters()))]
-    return float(loss), grads
+    return float(loss.detach()), grads
 
 
 def _rel(a, b):

@@ -77,7 +77,7 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
-template <int S>
+template <int S, int V>
 __global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __restrict__ q, const char* __restrict__ pimg,
                                                              const float* __restrict__ y, float* __restrict__ out,
                                                              float* __restrict__ partial, float* __restrict__ sinkbuf,
@@ -182,6 +182,7 @@ __global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __rest
   const uint64_t t0 = __builtin_amdgcn_s_memtime(), c0 = __builtin_amdgcn_s_memrealtime();
   for (int w = slot; w < ITEMS; w += G) {
     const bool has_next = w + G < ITEMS;
+    const bool early = (V & 2) && w != slot;  // the previous epilogue already issued this item's K tile 1 DMA
     const int it = w % NI, jt = w / NI;
 #pragma unroll
     for (int i = 0; i < TI; ++i)
@@ -197,7 +198,9 @@ __global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __rest
           for (int i = 0; i < TI; ++i) ypre[i] = *reinterpret_cast<const f32x4*>(y + (jb + fr) * LDO + ib + 16 * i + 4 * fg);
         }
       }
-      mfma_tile(0, [&] { dma_p(kt + 1, 1); });
+      mfma_tile(0, [&] {
+        if (!(early && kt == 0)) dma_p(kt + 1, 1);
+      });
       swrite(r1, 1);
       __syncthreads();
       gload(r1);
@@ -210,6 +213,9 @@ __global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __rest
       gload(r0);
     }
     if constexpr (S >= 4) {
+      // V & 2: the next item's K tile 1 weight DMA issued here, before the epilogue's loads and stores, so the
+      // next item's first barrier waits for it without waiting for the stores (vmcnt counts in issue order)
+      if ((V & 2) && has_next) dma_p(1, 1);
       float cs[TI][4];
 #pragma unroll
       for (int i = 0; i < TI; ++i) cs[i][0] = cs[i][1] = cs[i][2] = cs[i][3] = 0.f;
@@ -224,6 +230,7 @@ __global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __rest
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int64_t jg = jb + 16 * j + fr;
+        f32x4 vs[TI];
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
           f32x4 v = acc[i][j];
@@ -234,7 +241,34 @@ __global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __rest
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) cs[i][r] += v[r];
-          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + jg * LDO + ib + 16 * i + 4 * fg));
+          vs[i] = v;
+          if constexpr (!(V & 4)) {
+            if constexpr (V & 1) *reinterpret_cast<f32x4*>(out + jg * LDO + ib + 16 * i + 4 * fg) = v;
+            else __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(out + jg * LDO + ib + 16 * i + 4 * fg));
+          }
+        }
+        if constexpr (V & 4) {
+          // whole 128-B lines per row: tiles i and i + 1 of the same rows exchanged by a row rotation of 8 lanes,
+          // so one store covers 8 rows x 128 B (instead of 16 rows x 64 B)
+#pragma unroll
+          for (int i = 0; i < TI; i += 2) {
+            f32x4 A, B;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float xr = dpp_f32<0x128>(vs[i][r]), yr = dpp_f32<0x128>(vs[i + 1][r]);
+              A[r] = fr < 8 ? vs[i][r] : yr;
+              B[r] = fr < 8 ? xr : vs[i + 1][r];
+            }
+            const int64_t r0 = jb + 16 * j + (fr & 7);
+            const int col = ib + 16 * (i + (fr >> 3)) + 4 * fg;
+            if constexpr (V & 1) {
+              *reinterpret_cast<f32x4*>(out + r0 * LDO + col) = A;
+              *reinterpret_cast<f32x4*>(out + (r0 + 8) * LDO + col) = B;
+            } else {
+              __builtin_nontemporal_store(A, reinterpret_cast<f32x4*>(out + r0 * LDO + col));
+              __builtin_nontemporal_store(B, reinterpret_cast<f32x4*>(out + (r0 + 8) * LDO + col));
+            }
+          }
         }
       }
 #pragma unroll
@@ -279,10 +313,10 @@ struct Bufs {
   uint64_t* stamps;
 };
 
-template <int S>
+template <int S, int V = 0>
 static void run(const char* name, const Bufs& b) {
   auto launch = [&] {
-    hipLaunchKernelGGL(buildup_kernel<S>, dim3(GRID), dim3(THREADS), 0, 0, b.q, b.pimg, b.y, b.out, b.partial, b.sink,
+    hipLaunchKernelGGL((buildup_kernel<S, V>), dim3(GRID), dim3(THREADS), 0, 0, b.q, b.pimg, b.y, b.out, b.partial, b.sink,
                        b.stamps);
   };
   hipEvent_t e0, e1;
@@ -348,10 +382,16 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, (uint32_t*)b.y, ROWS * LDO, 2u, 0);
   hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, 0, (uint32_t*)b.pimg, (int64_t)NI * KTILES * IMG_P / 4, 3u, 1);
   CK(hipDeviceSynchronize());
-  bool want[6] = {true, true, true, true, true, true};
+  // arguments: stage numbers 0..5, or "v" for the stage-4/5 variants (V: 1 = plain stores instead of nontemporal,
+  // 2 = the next item's K tile 1 DMA before the epilogue)
+  bool want[6] = {true, true, true, true, true, true}, variants = false, lines = false;
   if (argc > 1) {
     for (int s = 0; s < 6; ++s) want[s] = false;
-    for (int a = 1; a < argc; ++a) want[atoi(argv[a]) % 6] = true;
+    for (int a = 1; a < argc; ++a) {
+      if (argv[a][0] == 'v') variants = true;
+      else if (argv[a][0] == 'l') lines = true;
+      else want[atoi(argv[a]) % 6] = true;
+    }
   }
   if (want[0]) run<0>("0 lds", b);
   if (want[1]) run<1>("1 +q", b);
@@ -359,5 +399,21 @@ int main(int argc, char** argv) {
   if (want[3]) run<3>("3 +dma", b);
   if (want[4]) run<4>("4 +store", b);
   if (want[5]) run<5>("5 +y (product work)", b);
+  if (variants) {
+    run<4, 1>("4 +store, plain stores", b);
+    run<4, 2>("4 +store, next K tile 1 DMA before the epilogue", b);
+    run<4, 3>("4 +store, plain stores + early DMA", b);
+    run<5, 0>("5 product work (again)", b);
+    run<5, 1>("5 +y, plain stores", b);
+    run<5, 2>("5 +y, next K tile 1 DMA before the epilogue", b);
+    run<5, 3>("5 +y, plain stores + early DMA", b);
+  }
+  if (lines) {
+    run<4, 4>("4 +store, 128-B line stores (nt)", b);
+    run<4, 5>("4 +store, 128-B line stores (plain)", b);
+    run<5, 4>("5 +y, 128-B line stores (nt)", b);
+    run<5, 5>("5 +y, 128-B line stores (plain)", b);
+    run<5, 6>("5 +y, 128-B line stores (nt) + early DMA", b);
+  }
   return 0;
 }

@@ -776,7 +776,7 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
         if constexpr (EPI == EPI_TANH || EPI == EPI_TANH_OUT) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = tanh_f32(v[r] + epi_lds[il + r]);
-          *reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig) = v;
+          acc[i][j] = v;  // stored below, two tiles per 128-B line store
           if constexpr (EPI == EPI_TANH_OUT) {
 #pragma unroll
             for (int o = 0; o < KO; ++o) {
@@ -795,9 +795,36 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
             v[r] = v[r] * fmaf(-yv[r], yv[r], 1.0f);
             cs[i][r] += v[r];
           }
-          __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig));
+          acc[i][j] = v;  // stored below, two tiles per 128-B line store
         } else {  // EPI_WGRAD: the split's partial
           *reinterpret_cast<f32x4*>(a.out + ((int64_t)sp * a.nj * BJ + jg) * a.ldo + ig) = v;
+        }
+      }
+      if constexpr (EPI == EPI_TANH || EPI == EPI_TANH_OUT || EPI == EPI_DTANH) {
+        // tiles i and i + 1 of rows jb + 16 j .. + 15 as 128-B line stores: a row rotation by 8 lanes trades the
+        // upper 8 rows of tile i for the lower 8 of tile i + 1, so each store writes 8 whole 128-B rows
+        // (32 consecutive features) instead of 16 half lines (backward 512 <- 256 2 % faster, forward alike;
+        // tools/x6_buildup.hip, profiles/r06d_x6_buildup_lines.log)
+#pragma unroll
+        for (int i = 0; i < TI; i += 2) {
+          f32x4 lo8, hi8;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float xr = dpp_f32<0x128>(acc[i][j][r]), yr = dpp_f32<0x128>(acc[i + 1][j][r]);
+            lo8[r] = fr < 8 ? acc[i][j][r] : yr;
+            hi8[r] = fr < 8 ? xr : acc[i + 1][j][r];
+          }
+          const int64_t r0 = (int64_t)jb + 16 * j + (fr & 7);
+          const int64_t col = (int64_t)it * BI + wi * C::WTI + 16 * (i + (fr >> 3)) + 4 * fg;
+          float* d0 = a.out + r0 * a.ldo + col;
+          float* d1 = a.out + (r0 + 8) * a.ldo + col;
+          if constexpr (EPI == EPI_DTANH) {
+            __builtin_nontemporal_store(lo8, reinterpret_cast<f32x4*>(d0));
+            __builtin_nontemporal_store(hi8, reinterpret_cast<f32x4*>(d1));
+          } else {
+            *reinterpret_cast<f32x4*>(d0) = lo8;
+            *reinterpret_cast<f32x4*>(d1) = hi8;
+          }
         }
       }
       if constexpr (EPI == EPI_TANH_OUT) {

@@ -63,6 +63,12 @@ int main() {
       {"0 + 1 + 0.75 ulp (C = 0)", 0.0f, 2, {1.0f, 0x1.8p-24f}},
       {"0 + 1 - 0.75 ulp(below) (C = 0)", 0.0f, 2, {1.0f, -0x1.8p-25f}},
       {"0 - 1 - 0.75 ulp (C = 0)", 0.0f, 2, {-1.0f, -0x1.8p-24f}},
+      {"C = +0.75 ulp, product 1", 0x1.8p-24f, 1, {1.0f}},
+      {"C = -0.375 ulp, product 1", -0x1.8p-25f, 1, {1.0f}},
+      {"C = +0.375 ulp, product 1", 0x1.8p-25f, 1, {1.0f}},
+      {"C = -0.75 ulp, product -1", -0x1.8p-24f, 1, {-1.0f}},
+      {"C = +2^-30, product 1", 0x1.0p-30f, 1, {1.0f}},
+      {"C = -2^-30, product 1", -0x1.0p-30f, 1, {1.0f}},
       {"1 + 2^-30 (far below)", 1.0f, 1, {0x1.0p-30f}},
       {"1 - 2^-30 (far below)", 1.0f, 1, {-0x1.0p-30f}},
       {"-1 + 2^-30 (far below)", -1.0f, 1, {0x1.0p-30f}},

@@ -8,6 +8,10 @@
 //   2 three accumulators (hi.hi | mid.hi + hi.mid | lo.hi + hi.lo + mid.mid), added at the end in fp32
 //   3 a fresh accumulator per K step (the six products), added to the running sum in fp32 (RNE)
 //   4 the split without the lo plane's products (hi.hi, mid.hi, hi.mid, mid.mid)
+//   5 the five smaller products of a K step into a fresh accumulator, added to the running sum in fp32,
+//     then hi.hi into the running sum (one temporary per output tile)
+//   6 two accumulators: hi.hi | the five smaller products, added at the end
+//   7 the five smaller products into the running sum, hi.hi into a zero accumulator added in fp32 per K step
 // and reports, against an fp64 GEMM of the same inputs: offset = mean(e) / rms(e), colsum = relative error of
 // the column sums, elem = relative Frobenius error.
 //
@@ -25,7 +29,7 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int M = 65536, N = 256, K = 256;
+static int M = 65536, N = 256, K = 256;  // PROBE_M / PROBE_N / PROBE_K override
 
 __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
   const bf16x2 v = {(__bf16)a, (__bf16)b};
@@ -50,7 +54,8 @@ __device__ __forceinline__ f32x4 mf(u32x4 a, u32x4 b, f32x4 c) {
 
 // C[m][n] = sum_k A[m][k] B[n][k]  (both K-contiguous); one wave per 16 x 16 tile
 template <int V>
-__global__ __launch_bounds__(64) void x6_tile(const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C) {
+__global__ __launch_bounds__(64) void x6_tile(const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C,
+                                              int M, int N, int K) {
   const int l = threadIdx.x, tm = blockIdx.x, tn = blockIdx.y;
   const int r = l & 15, g = l >> 4;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f}, a2 = acc, a3 = acc;
@@ -78,17 +83,31 @@ __global__ __launch_bounds__(64) void x6_tile(const float* __restrict__ A, const
       t = mf(al, bh, t); t = mf(ah, bl, t); t = mf(am, bm, t);
       t = mf(am, bh, t); t = mf(ah, bm, t); t = mf(ah, bh, t);
       for (int i = 0; i < 4; ++i) acc[i] += t[i];
-    } else {
+    } else if constexpr (V == 4) {
       acc = mf(am, bm, acc); acc = mf(am, bh, acc); acc = mf(ah, bm, acc); acc = mf(ah, bh, acc);
+    } else if constexpr (V == 5) {
+      f32x4 t = {0.f, 0.f, 0.f, 0.f};
+      t = mf(al, bh, t); t = mf(ah, bl, t); t = mf(am, bm, t); t = mf(am, bh, t); t = mf(ah, bm, t);
+      for (int i = 0; i < 4; ++i) acc[i] += t[i];
+      acc = mf(ah, bh, acc);
+    } else if constexpr (V == 7) {
+      acc = mf(al, bh, acc); acc = mf(ah, bl, acc); acc = mf(am, bm, acc); acc = mf(am, bh, acc); acc = mf(ah, bm, acc);
+      const f32x4 t = mf(ah, bh, (f32x4){0.f, 0.f, 0.f, 0.f});
+      for (int i = 0; i < 4; ++i) acc[i] += t[i];
+    } else {
+      a2 = mf(al, bh, a2); a2 = mf(ah, bl, a2); a2 = mf(am, bm, a2); a2 = mf(am, bh, a2); a2 = mf(ah, bm, a2);
+      acc = mf(ah, bh, acc);
     }
   }
   if constexpr (V == 2)
     for (int i = 0; i < 4; ++i) acc[i] = acc[i] + (a2[i] + a3[i]);
+  if constexpr (V == 6)
+    for (int i = 0; i < 4; ++i) acc[i] = acc[i] + a2[i];
   // accumulator lane l: rows 4 g .. + 3 (of A's 16), column r (of B's 16)
   for (int i = 0; i < 4; ++i) C[(int64_t)(tm * 16 + 4 * g + i) * N + tn * 16 + r] = acc[i];
 }
 
-__global__ void ref64(const float* __restrict__ A, const float* __restrict__ B, double* __restrict__ C) {
+__global__ void ref64(const float* __restrict__ A, const float* __restrict__ B, double* __restrict__ C, int M, int N, int K) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)M * N) return;
   const int m = (int)(idx / N), n = (int)(idx % N);
@@ -109,7 +128,7 @@ static double normal(uint64_t& s) {  // Box-Muller on xorshift
 
 template <int V>
 static void run(const char* name, const float* dA, const float* dB, float* dC, const std::vector<double>& ref) {
-  hipLaunchKernelGGL(x6_tile<V>, dim3(M / 16, N / 16), dim3(64), 0, 0, dA, dB, dC);
+  hipLaunchKernelGGL(x6_tile<V>, dim3(M / 16, N / 16), dim3(64), 0, 0, dA, dB, dC, M, N, K);
   std::vector<float> c((size_t)M * N);
   (void)hipMemcpy(c.data(), dC, c.size() * 4, hipMemcpyDeviceToHost);
   double se = 0, se2 = 0, sr2 = 0, cs2 = 0, csr2 = 0;
@@ -133,6 +152,10 @@ static void run(const char* name, const float* dA, const float* dB, float* dC, c
 }
 
 int main() {
+  if (getenv("PROBE_M")) M = atoi(getenv("PROBE_M"));
+  if (getenv("PROBE_N")) N = atoi(getenv("PROBE_N"));
+  if (getenv("PROBE_K")) K = atoi(getenv("PROBE_K"));
+  printf("{\"M\": %d, \"N\": %d, \"K\": %d}\n", M, N, K);
   std::vector<float> a((size_t)M * K), b((size_t)N * K);
   uint64_t s = 0x9E3779B97F4A7C15ull;
   for (auto& v : a) v = (float)(normal(s) * 1e-3);
@@ -145,7 +168,7 @@ int main() {
   (void)hipMalloc(&dR, (size_t)M * N * 8);
   (void)hipMemcpy(dA, a.data(), a.size() * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(dB, b.data(), b.size() * 4, hipMemcpyHostToDevice);
-  hipLaunchKernelGGL(ref64, dim3((M * N + 255) / 256), dim3(256), 0, 0, dA, dB, dR);
+  hipLaunchKernelGGL(ref64, dim3((M * N + 255) / 256), dim3(256), 0, 0, dA, dB, dR, M, N, K);
   std::vector<double> ref((size_t)M * N);
   (void)hipMemcpy(ref.data(), dR, ref.size() * 8, hipMemcpyDeviceToHost);
   run<0>("0 kernel order, one accumulator", dA, dB, dC, ref);
@@ -153,5 +176,8 @@ int main() {
   run<2>("2 three accumulators by magnitude", dA, dB, dC, ref);
   run<3>("3 fresh accumulator per K step + fp32 add", dA, dB, dC, ref);
   run<4>("4 without the lo-plane products", dA, dB, dC, ref);
+  run<5>("5 smaller products into a fresh accumulator per K step, fp32 add, then hi.hi", dA, dB, dC, ref);
+  run<6>("6 two accumulators: hi.hi | the smaller five", dA, dB, dC, ref);
+  run<7>("7 smaller five into the running sum, hi.hi into a zero accumulator + fp32 add", dA, dB, dC, ref);
   return 0;
 }

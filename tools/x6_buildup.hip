@@ -162,14 +162,59 @@ __global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __rest
     __builtin_amdgcn_sched_barrier(0);
     constexpr int PP[6] = {2, 0, 1, 1, 0, 0};
     constexpr int QP[6] = {0, 2, 1, 0, 1, 0};
+    if constexpr (V & 8) {
+      // split accumulation (tools/x6_accum_probe.hip variant 5): per output tile the five smaller products into
+      // a fresh temporary, added to the running sum in fp32, then hi.hi into it; 4 tiles (one row i) at a time
 #pragma unroll
-    for (int x = 0; x < 6; ++x)
+      for (int i = 0; i < TI; ++i) {
+        f32x4 t[TJ];
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+        for (int j = 0; j < TJ; ++j) t[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int x = 0; x < 5; ++x)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            t[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pf[PP[x]][i]),
+                                                           __builtin_bit_cast(bf16x8, qf[QP[x]][j]), t[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          acc[i][j] += t[j];
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pf[0][i]),
+                                                              __builtin_bit_cast(bf16x8, qf[0][j]), acc[i][j], 0, 0, 0);
+        }
+      }
+    } else if constexpr (V & 16) {
+      // hi.hi into fresh temporaries (tools/x6_accum_probe.hip variant 7): the five smaller products into the
+      // running sum as before (their sums are far below it: added exactly, then rounded), hi.hi into a zero
+      // accumulator and added in fp32 -- no MFMA ever aligns the running sum to larger products
+#pragma unroll
+      for (int x = 0; x < 5; ++x)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pf[PP[x]][i]),
+                                                                __builtin_bit_cast(bf16x8, qf[QP[x]][j]), acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        f32x4 t[TJ];
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pf[PP[x]][i]),
-                                                              __builtin_bit_cast(bf16x8, qf[QP[x]][j]), acc[i][j], 0, 0, 0);
+          t[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pf[0][i]), __builtin_bit_cast(bf16x8, qf[0][j]),
+                                                         (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] += t[j];
+      }
+    } else {
+#pragma unroll
+      for (int x = 0; x < 6; ++x)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, pf[PP[x]][i]),
+                                                                __builtin_bit_cast(bf16x8, qf[QP[x]][j]), acc[i][j], 0, 0, 0);
+    }
   };
 
   u32x4 r0[2] = {}, r1[2] = {};
@@ -384,12 +429,13 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   // arguments: stage numbers 0..5, or "v" for the stage-4/5 variants (V: 1 = plain stores instead of nontemporal,
   // 2 = the next item's K tile 1 DMA before the epilogue)
-  bool want[6] = {true, true, true, true, true, true}, variants = false, lines = false;
+  bool want[6] = {true, true, true, true, true, true}, variants = false, lines = false, split = false;
   if (argc > 1) {
     for (int s = 0; s < 6; ++s) want[s] = false;
     for (int a = 1; a < argc; ++a) {
       if (argv[a][0] == 'v') variants = true;
       else if (argv[a][0] == 'l') lines = true;
+      else if (argv[a][0] == 's') split = true;
       else want[atoi(argv[a]) % 6] = true;
     }
   }
@@ -407,6 +453,16 @@ int main(int argc, char** argv) {
     run<5, 1>("5 +y, plain stores", b);
     run<5, 2>("5 +y, next K tile 1 DMA before the epilogue", b);
     run<5, 3>("5 +y, plain stores + early DMA", b);
+  }
+  if (split) {
+    run<0, 8>("0 lds, split accumulation", b);
+    run<3, 8>("3 +dma, split accumulation", b);
+    run<5, 0>("5 product work", b);
+    run<5, 8>("5 product work, split accumulation", b);
+    run<5, 12>("5 product work, split accumulation + 128-B line stores", b);
+    run<5, 4>("5 product work, 128-B line stores", b);
+    run<0, 16>("0 lds, hi.hi into fresh temporaries", b);
+    run<5, 20>("5 product work, hi.hi into fresh temporaries + 128-B line stores", b);
   }
   if (lines) {
     run<4, 4>("4 +store, 128-B line stores (nt)", b);

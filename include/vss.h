@@ -327,7 +327,7 @@ int vss_output_backward(void* stream, int64_t rows, int32_t k_pad, int32_t n, co
                         const float* y, float* grad_in, float* bias_partial, float* wgrad_partial);
 
 /* vss_output_backward_direct: the same pass for the update's minibatch without autograd
- * (ppo_continuous_action_isaacgym.py direct_minibatch): g_out (rows, k_out) as vss_ppo_loss_direct
+ * (vss_amd/minibatch.py direct_minibatch): g_out (rows, k_out) as vss_ppo_loss_direct
  * writes it and w_out (k_out, n) as nn.Linear holds it -- no padded copies; k_out in {1, 2, 3, 4, 6, 8},
  * n in {128, 256, 512, 1024}.  bias_partial (chunks, n), wgrad_partial (chunks, k_out, n) with chunks =
  * vss_output_backward_direct_chunks(rows, k_out, n) <= 256 (-1 for a bad shape), few enough for one
@@ -447,7 +447,7 @@ int vss_ppo_loss(void* stream, int64_t rows, int64_t rows_pad, int32_t n_act, co
                  float* grad_logstd, float* loss_out, float* stats_out, float* partial);
 
 /* vss_ppo_loss_direct: the same loss for the update's minibatch without autograd
- * (ppo_continuous_action_isaacgym.py direct_minibatch), from what the networks' last launches leave:
+ * (vss_amd/minibatch.py direct_minibatch), from what the networks' last launches leave:
  *   mean_parts (mean_nparts, rows_pad, n_act) + mean_bias (n_act,): the actor's output as the parts of
  *     vss_linear_tanh_out_bf16x6's out_part (summed in order, then the bias); value_parts
  *     (value_nparts, rows_pad) + value_bias (1,) the critic's;
@@ -501,8 +501,8 @@ int vss_minibatch_gather(void* stream, int64_t mb, int64_t rows_pad, int64_t bat
 int vss_adv_part_sum(void* stream, int32_t nparts, const double* part, double* out);
 
 /* ---------------------------------------------------------------------------------------------
- * The update's gradient bookkeeping on flat buffers (csrc/vss_optim.hip; ppo_continuous_action_isaacgym.py
- * FlatParams / FlatGrads / FlatAdam).  Replaces, per minibatch, nn.utils.clip_grad_norm_ (ppo…:353)
+ * The update's gradient bookkeeping on flat buffers (csrc/vss_optim.hip; vss_amd/flat.py
+ * FlatGrads / FlatAdam).  Replaces, per minibatch, nn.utils.clip_grad_norm_ (ppo…:353)
  * and optim.Adam(eps=1e-5).step() (ppo…:166,354) -- torch's per-tensor norm chain and multi-tensor
  * Adam -- with two launches, and the split GEMMs' torch.sum reductions with one launch per backward.
  *

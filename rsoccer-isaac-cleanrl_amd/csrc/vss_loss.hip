@@ -77,7 +77,7 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 }
 
 // (sum, sum of squares) parts of the advantages -> (mean, std) as fp32, the fp64 formula of
-// normalize_advantages' all-reduced branch (ppo_continuous_action_isaacgym.py): mean = s / n,
+// normalize_advantages' all-reduced branch (vss_amd/minibatch.py): mean = s / n,
 // std = sqrt(max((q - n mean mean) / (n - 1), 0)).  Every block the same fixed order: wave 0's lanes
 // take parts lane, lane + 64, ..., then the wave sum; the result is shared through LDS.
 __device__ __forceinline__ void adv_moments(const double* part, int nparts, double n, float& mean, float& std) {

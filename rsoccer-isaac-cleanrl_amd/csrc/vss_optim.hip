@@ -3,7 +3,7 @@
 // SURVEY §8 A13 (ppo_continuous_action_isaacgym.py:351-354): after loss.backward() the reference clips the
 // gradient norm (nn.utils.clip_grad_norm_, ppo…:353) and steps Adam (optim.Adam(eps=1e-5), ppo…:166,354).
 // Here every parameter and every gradient of the Agent lives in one flat fp32 buffer
-// (ppo_continuous_action_isaacgym.py FlatParams / FlatGrads), so both are two launches over 1.07 M floats
+// (vss_amd/flat.py FlatGrads / FlatAdam), so both are two launches over 1.07 M floats
 // instead of torch's per-tensor norm chain + multi-tensor Adam (~8 launches, ~130 us per minibatch at the
 // reference's 4,095 envs, profiles/r05_ppo_4095_minibatch_window.txt):
 //

@@ -114,7 +114,7 @@ def ppo_loss(mean, logstd, value, action, logprob_old, adv, returns, values_old,
     return loss, tuple(stats[i] for i in range(6))
 
 
-# ---- the update's minibatch without autograd (ppo_continuous_action_isaacgym.py direct_minibatch) -------
+# ---- the update's minibatch without autograd (vss_amd/minibatch.py direct_minibatch) -------
 
 def ppo_loss_direct(mean_parts, mean_bias, value_parts, value_bias, logstd, action, logprob_old, adv, adv_part,
                     adv_count, returns, values_old, clip_coef, ent_coef, vf_coef, clip_vloss, grad_logstd,

@@ -92,9 +92,10 @@ def _rel(a, b):
 # negative bias per MFMA that grows like K^1.5 with the contraction length, while an unbiased error grows like
 # K^0.5 -- the weight gradients contract over 65,536 rows per split and the bias gradients sum 2 M column entries.
 # Keeping the hi.hi products in an accumulator of their own removes it (tools/x6_accum_probe.hip variants 2 / 6)
-# but needs 64 more registers than two waves per SIMD leave.
+# but needs 64 more registers than two waves per SIMD leave.  torch's own fp32 error at 2 M rows
+# reaches 1.85e-5 for a weight matrix on this data (profiles/r06k_pytest_gpu.log), hence the 5e-5 cap there.
 BOUNDS = {131040: dict(overall=1.25, matrix=1.25, small_matrix=2.0, abs=1e-5, bias=3e-5),
-          2097152: dict(overall=1.6, matrix=2.0, small_matrix=2.0, abs=2e-5, bias=1e-4)}
+          2097152: dict(overall=1.6, matrix=2.0, small_matrix=2.0, abs=5e-5, bias=1e-4)}
 
 
 @pytest.mark.gpu

@@ -776,7 +776,7 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
         if constexpr (EPI == EPI_TANH || EPI == EPI_TANH_OUT) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = tanh_f32(v[r] + epi_lds[il + r]);
-          acc[i][j] = v;  // stored below, two tiles per 128-B line store
+          *reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ig) = v;
           if constexpr (EPI == EPI_TANH_OUT) {
 #pragma unroll
             for (int o = 0; o < KO; ++o) {
@@ -800,11 +800,12 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
           *reinterpret_cast<f32x4*>(a.out + ((int64_t)sp * a.nj * BJ + jg) * a.ldo + ig) = v;
         }
       }
-      if constexpr (EPI == EPI_TANH || EPI == EPI_TANH_OUT || EPI == EPI_DTANH) {
+      if constexpr (EPI == EPI_DTANH) {
         // tiles i and i + 1 of rows jb + 16 j .. + 15 as 128-B line stores: a row rotation by 8 lanes trades the
-        // upper 8 rows of tile i for the lower 8 of tile i + 1, so each store writes 8 whole 128-B rows
-        // (32 consecutive features) instead of 16 half lines (backward 512 <- 256 2 % faster, forward alike;
-        // tools/x6_buildup.hip, profiles/r06d_x6_buildup_lines.log)
+        // upper 8 rows of tile i for the lower 8 of tile i + 1, so each nontemporal store writes 8 whole 128-B
+        // rows (32 consecutive features) instead of 16 half lines: backward 512 <- 256 3.23 vs 3.28 ms, update
+        // 2.227 vs 2.236 s (same-box A/B, profiles/r06l_lines_ab.log).  The forwards' plain stores keep one tile
+        // per store: as line stores the forward 512 -> 512 ran 2.5 % slower (5.15 vs 5.02 ms, same A/B).
 #pragma unroll
         for (int i = 0; i < TI; i += 2) {
           f32x4 lo8, hi8;

@@ -21,8 +21,14 @@
 // 100 MHz around each wave's item loop, median over waves; MI355X_MICROARCH.md DVFS item 6) and the matrix
 // pipes' busy fraction implied by them (bf16 FLOP / (clock x 1024 FLOP per SIMD-cycle x 1024 SIMDs)).
 //
+// Variants of a stage (template V, bits): 1 plain instead of nontemporal epilogue stores; 2 the next item's K tile 1
+// weight DMA issued before the epilogue; 4 two MFMA tiles per store as 8 whole 128-B rows (kept in the product);
+// 8 the five smaller products into a per-row-of-tiles temporary added in fp32 (numerics variant 5 of
+// tools/x6_accum_probe.hip); 16 hi.hi into fresh temporaries (variant 7).
+//
 //   hipcc -O3 --offload-arch=gfx950 -o tools/_build/x6_buildup tools/x6_buildup.hip
-//   tools/_build/x6_buildup [stage ...]    -> one JSON line per stage
+//   tools/_build/x6_buildup [stage ...] [v] [l] [s]    -> one JSON line per stage / variant
+//   (v: the store / DMA-order variants, l: the line-store variants, s: the accumulation variants)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -25,19 +25,36 @@ def launch():
     U.linear_tanh_backward_x6(gn, w, y, out=out, planes=planes, defer=[])
 
 
-e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-for seconds, timed in ((1.0, False), (2.0, True)):
-    launches, ms = 0, 0.0
-    e0.record()
-    while ms < seconds * 1e3:
-        for _ in range(10):
-            launch()
-        launches += 10
-        e1.record()
-        e1.synchronize()
-        ms = e0.elapsed_time(e1)
-per = ms / launches
+
+
+def timed(fn):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for seconds in (1.0, 2.0):
+        launches, ms = 0, 0.0
+        e0.record()
+        while ms < seconds * 1e3:
+            for _ in range(10):
+                fn()
+            launches += 10
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+    return launches, ms / launches
+
+
+launches, per = timed(launch)
 tf = 2.0 * rows * n * k_next / (per * 1e-3) / 1e12
 print(json.dumps({"stage": "product vss_linear_tanh_backward_bf16x6 512<-256", "launches": launches, "ms_per_launch": per,
                   "x6_tflops": tf, "frac_of_x6_peak": tf / (2500.0 / 6),
                   "note": "wall includes the defer=[] partial-sum path (no reduction launch) per call"}), flush=True)
+# the forward 512 -> 512 (the bench's update_gemm_roofline shape)
+del gn, out
+x = torch.tanh(torch.randn(rows, 512, device="cuda", generator=g))
+w2 = torch.randn(512, 512, device="cuda", generator=g) / 512 ** 0.5
+b2 = torch.zeros(512, device="cuda")
+y2 = torch.empty(rows, 512, device="cuda")
+p2 = U.weight_planes([(w2, False)])[0]
+launches, per = timed(lambda: U.linear_tanh_x6(x, w2, b2, out=y2, planes=p2))
+tf = 2.0 * rows * 512 * 512 / (per * 1e-3) / 1e12
+print(json.dumps({"stage": "product vss_linear_tanh_bf16x6 512->512", "launches": launches, "ms_per_launch": per,
+                  "x6_tflops": tf, "frac_of_x6_peak": tf / (2500.0 / 6)}), flush=True)

@@ -764,3 +764,16 @@ def test_train_amp_bf16_option_gpu(tmp_path):
     for h in hist:
         for k in ("v_loss", "pg_loss", "entropy", "approx_kl"):
             assert np.isfinite(h[k]), (k, h)
+
+
+def test_drop_in_script_keeps_the_reference_shape():
+    """The drop-in script is the reference's outline -- argparse, Agent, the loop (ppo…:1-460) -- with the update
+    machinery in vss_amd/ (round-5 VERDICT Next 6): at most 600 lines, and the only classes it defines are the
+    reference's Agent and ExtractObsWrapper."""
+    import ast
+    src = open(P.__file__).read()
+    assert len(src.splitlines()) <= 600
+    classes = [n.name for n in ast.parse(src).body if isinstance(n, ast.ClassDef)]
+    assert classes == ["Agent", "ExtractObsWrapper"], classes
+    for name in ("FlatGrads", "FlatAdam", "MinibatchGraph", "DirectRows", "EpochPermutations", "TerminalValues"):
+        assert getattr(P, name, None) is None or getattr(P, name).__module__.startswith("vss_amd."), name

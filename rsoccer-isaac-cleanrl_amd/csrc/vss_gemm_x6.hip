@@ -376,6 +376,38 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += dpp_f32<0x140>(v);
   return v;
 }
+// v summed over the four rows of 16 lanes (an MFMA output column's k groups fg): v + v of lane ^ 16, then +
+// that of lane ^ 32 -- the pairs and the bits of __shfl_xor 16 / 32, by v_permlane16_swap / v_permlane32_swap
+// instead of two LDS round trips
+__device__ __forceinline__ float kgroup_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+// sum over the 64 lanes, every lane getting the same bits (each step adds a pair in an order-free way)
+__device__ __forceinline__ float wave64_sum(float v) { return kgroup_sum(row16_sum(v)); }
+// m's bit for this lane ? b : a, as one v_cndmask_b32 (written as C selects over an array, the tree below is
+// turned into a scratch-indexed load)
+__device__ __forceinline__ float lane_sel(uint64_t m, float a, float b) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+  return r;
+}
+// t[k] for k = the lane's index (0 .. 15) by a select tree on its bits (no exec-mask branch): after row16_sum
+// every lane of a row holds every sum, so lane k can write the k-th one
+__device__ __forceinline__ float pick16(const float (&t)[16], int k) {
+  const uint64_t m0 = __builtin_amdgcn_ballot_w64(k & 1), m1 = __builtin_amdgcn_ballot_w64(k & 2),
+                 m2 = __builtin_amdgcn_ballot_w64(k & 4), m3 = __builtin_amdgcn_ballot_w64(k & 8);
+  float a[8], b[4], c[2];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) a[m] = lane_sel(m0, t[2 * m], t[2 * m + 1]);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) b[m] = lane_sel(m1, a[2 * m], a[2 * m + 1]);
+#pragma unroll
+  for (int m = 0; m < 2; ++m) c[m] = lane_sel(m2, b[2 * m], b[2 * m + 1]);
+  return lane_sel(m3, c[0], c[1]);
+}
 
 template <int EPI, int SP, int SQ, class C, int KO = 0>
 __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
@@ -563,6 +595,31 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
   auto loss_epilogue = [&](f32x4 (&ac)[TI][TJ], int it, int jt) __attribute__((always_inline)) {
     if constexpr (LOSS) {
       const int ib = it * BI + wi * C::WTI;
+      // phase 2's inputs, requested before phase 1 (waves 0 and 1: one thread per row) so that their latency
+      // hides behind phase 1's tanh and output sums instead of stalling the two waves after its barrier
+      const int64_t grow = (int64_t)jt * BJ + tid;
+      const bool row_real = tid < BJ && grow < a.rows_real;
+      float in_x[KO], in_b[KO], in_ls[KO], in_a = 0.f, in_l = 0.f;
+#pragma unroll
+      for (int o = 0; o < KO; ++o) in_x[o] = in_b[o] = in_ls[o] = 0.f;
+      if (tid < BJ) {
+#pragma unroll
+        for (int o = 0; o < KO; ++o) {
+          in_b[o] = a.b_out[o];
+          if constexpr (EPI == EPI_LOSS_A) in_ls[o] = a.logstd[o];
+        }
+        if (row_real) {
+          if constexpr (EPI == EPI_LOSS_A) {
+#pragma unroll
+            for (int o = 0; o < KO; ++o) in_x[o] = a.l_act[grow * KO + o];
+            in_a = a.l_adv[grow];
+            in_l = a.l_logp[grow];
+          } else {
+            in_a = a.l_ret[grow];
+            in_l = a.clip_vloss ? a.l_val[grow] : 0.f;
+          }
+        }
+      }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int rl = wj * C::WTJ + 16 * j + fr;  // row within the item
@@ -588,36 +645,31 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
         }
 #pragma unroll
         for (int o = 0; o < KO; ++o) {
-          float d = od[o];
-          d += __shfl_xor(d, 16);
-          d += __shfl_xor(d, 32);
+          const float d = kgroup_sum(od[o]);
           if (fg == 0) epi_lds[E_P + (wi * BJ + rl) * KO + o] = d;
         }
       }
       __syncthreads();
       if (tid < BJ) {  // waves 0 and 1 whole: one thread per row of the item
-        const int64_t grow = (int64_t)jt * BJ + tid;
         float outv[KO], g[KO], t[kLossStats > 0 ? 5 + 2 * KO : 1];
 #pragma unroll
         for (int o = 0; o < KO; ++o) {
           float d = epi_lds[E_P + tid * KO + o];
 #pragma unroll
           for (int q = 1; q < C::WI; ++q) d += epi_lds[E_P + (q * BJ + tid) * KO + o];
-          outv[o] = d + a.b_out[o];
+          outv[o] = d + in_b[o];
           g[o] = 0.f;
         }
 #pragma unroll
         for (int k = 0; k < 5 + 2 * KO; ++k) t[k] = 0.f;
-        if (grow < a.rows_real) {
+        if (row_real) {
           if constexpr (EPI == EPI_LOSS_A) {
-            float var[KO], lsc[KO], x[KO], gm[KO], lg[KO];
-            vlossrow::actor_consts<KO>(a.logstd, var, lsc);
-#pragma unroll
-            for (int o = 0; o < KO; ++o) x[o] = a.l_act[grow * KO + o];
-            float A = a.l_adv[grow];
+            float var[KO], lsc[KO], gm[KO], lg[KO];
+            vlossrow::actor_consts<KO>(in_ls, var, lsc);
+            float A = in_a;
             if (a.adv_part) A = (A - epi_lds[E_AD]) / (epi_lds[E_AD + 1] + 1e-8f);
-            vlossrow::actor_row<KO>(outv, x, a.l_logp[grow], A, var, lsc, a.clip, a.clip_lo, a.clip_hi, a.inv_n, t[0],
-                                    t[2], t[3], t[4], gm, lg);
+            vlossrow::actor_row<KO>(outv, in_x, in_l, A, var, lsc, a.clip, a.clip_lo, a.clip_hi, a.inv_n, t[0], t[2],
+                                    t[3], t[4], gm, lg);
 #pragma unroll
             for (int o = 0; o < KO; ++o) {
               g[o] = gm[o];
@@ -626,8 +678,7 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
             }
           } else {
             float gv;
-            vlossrow::critic_row(outv[0], a.l_ret[grow], a.clip_vloss ? a.l_val[grow] : 0.f, a.clip_vloss, a.clip,
-                                 a.vf_coef, a.inv_n, t[1], gv);
+            vlossrow::critic_row(outv[0], in_a, in_l, a.clip_vloss, a.clip, a.vf_coef, a.inv_n, t[1], gv);
             g[0] = gv;
             t[5] = gv;
           }
@@ -635,13 +686,12 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
         // the row gradient over this row's first output part (read above by this thread only)
 #pragma unroll
         for (int o = 0; o < KO; ++o) epi_lds[E_P + tid * KO + o] = g[o];
+        // the terms summed over the wave (every lane gets every sum), lane k adding the k-th into its slot
+        float ts[16];
 #pragma unroll
-        for (int k = 0; k < 5 + 2 * KO; ++k) {
-          float v = t[k];
-#pragma unroll
-          for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
-          if (lane == 0) epi_lds[E_ST + wv * kLossStats + k] += v;
-        }
+        for (int k = 0; k < 16; ++k) ts[k] = k < 5 + 2 * KO ? wave64_sum(t[k]) : 0.f;
+        const float tv = pick16(ts, fr);
+        if (lane < 5 + 2 * KO) epi_lds[E_ST + wv * kLossStats + lane] += tv;
       }
       __syncthreads();
       // feature group by feature group (i outer): 4 + 4 KO sums live, not TI times that
@@ -674,16 +724,21 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
           }
           __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(a.out + jg * a.ldo + ib + 16 * i + 4 * fg));
         }
+        // the 4 + 4 KO sums over the 16 rows, lane fr adding the fr-th into its slot: one read-modify-write
+        // of distinct words per feature group, not 4 + 4 KO serial ones by lane 0 of each row
+        float t[16];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int f = il + r;
-          const float tc = row16_sum(cs[r]);
-          if (fr == 0) epi_lds[E_CS + wj * BI + f] += tc;
+          t[r] = row16_sum(cs[r]);
 #pragma unroll
-          for (int o = 0; o < KO; ++o) {
-            const float td = row16_sum(dw[r][o]);
-            if (fr == 0) epi_lds[E_DW + (wj * KO + o) * BI + f] += td;
-          }
+          for (int o = 0; o < KO; ++o) t[4 + 4 * o + r] = row16_sum(dw[r][o]);
+        }
+#pragma unroll
+        for (int k = 4 + 4 * KO; k < 16; ++k) t[k] = 0.f;
+        const float v = pick16(t, fr);
+        if (fr < 4 + 4 * KO) {
+          const int slot = fr < 4 ? E_CS + wj * BI + il + fr : E_DW + (wj * KO + ((fr - 4) >> 2)) * BI + il + (fr & 3);
+          epi_lds[slot] += v;
         }
       }
     }
@@ -832,23 +887,22 @@ __global__ __launch_bounds__(C::THREADS, C::BPC) void gemm_x6_kernel(Args a) {
         // the wave's 64-feature slice of the output layer for row jg: the 4 k groups' lanes
 #pragma unroll
         for (int o = 0; o < KO; ++o) {
-          float d = od[o];
-          d += __shfl_xor(d, 16);
-          d += __shfl_xor(d, 32);
+          const float d = kgroup_sum(od[o]);
           if (fg == 0) a.out_part[(((int64_t)ib >> 6) * (a.nj * BJ) + jg) * KO + o] = d;
         }
       }
     }
     if constexpr (EPI == EPI_DTANH) {
-      // the 16 rows (lanes fr) of each k group, added to the wave's (wj, feature) slot: one lane
-      // per slot, so no two lanes ever add into the same word
+      // the 16 rows (lanes fr) of each k group, added to the wave's (wj, feature) slots: lane fr adds the
+      // sum of feature 16 (fr >> 2) + 4 fg + (fr & 3), so the 64 lanes update the wave's 64 slots in one
+      // read-modify-write of distinct words (not 16 serial ones by lane 0 of each row)
+      static_assert(EPI != EPI_DTANH || TI == 4, "EPI_DTANH column sums: 4 feature tiles per wave");
+      float t[16];
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float t = row16_sum(cs[i][r]);
-          if (fr == 0) epi_lds[wj * BI + wi * C::WTI + 16 * i + 4 * fg + r] += t;
-        }
+        for (int r = 0; r < 4; ++r) t[4 * i + r] = row16_sum(cs[i][r]);
+      epi_lds[wj * BI + wi * C::WTI + 16 * (fr >> 2) + 4 * fg + (fr & 3)] += pick16(t, fr);
     }
     if (!has_next) break;
     w = next;

@@ -321,8 +321,8 @@ def test_randperm_ties_are_shuffled_at_batch_size_gpu():
 @pytest.mark.parametrize("hip", [True, False])
 def test_epoch_permutations_gpu(hip, monkeypatch):
     """EpochPermutations on the GPU (side stream, drawn one epoch ahead): every epoch a permutation of the
-    batch, the same sequence for the same generator seed; with VSS_RANDPERM=torch exactly torch.randperm's
-    sequence from that generator."""
+    batch, the same sequence for the same generator seed; without VSS_RANDPERM=hip (the default) exactly
+    torch.randperm's sequence from that generator."""
     monkeypatch.setattr(MB, "RANDPERM_HIP", hip)
     batch, epochs = 100000, 4
 

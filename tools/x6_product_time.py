@@ -58,3 +58,30 @@ launches, per = timed(lambda: U.linear_tanh_x6(x, w2, b2, out=y2, planes=p2))
 tf = 2.0 * rows * 512 * 512 / (per * 1e-3) / 1e12
 print(json.dumps({"stage": "product vss_linear_tanh_bf16x6 512->512", "launches": launches, "ms_per_launch": per,
                   "x6_tflops": tf, "frac_of_x6_peak": tf / (2500.0 / 6)}), flush=True)
+# the fused loss launches (the last hidden layer 512 -> 256 with the output layer and the loss, EPI_LOSS_A /
+# EPI_LOSS_C) beside the plain forward 512 -> 256 of the same shape: what the loss epilogue costs per launch
+del y2
+x3 = x
+w3 = torch.randn(256, 512, device="cuda", generator=g) / 512 ** 0.5
+b3 = torch.zeros(256, device="cuda")
+p3 = U.weight_planes([(w3, False)])[0]
+y3 = torch.empty(rows, 256, device="cuda")
+launches, per = timed(lambda: U.linear_tanh_x6(x3, w3, b3, out=y3, planes=p3))
+tf = 2.0 * rows * 256 * 512 / (per * 1e-3) / 1e12
+print(json.dumps({"stage": "product vss_linear_tanh_bf16x6 512->256", "launches": launches, "ms_per_launch": per,
+                  "x6_tflops": tf, "frac_of_x6_peak": tf / (2500.0 / 6)}), flush=True)
+del y3
+real = rows - 32  # padding rows at the end, as a padded minibatch has
+act = torch.randn(rows, 2, device="cuda", generator=g) * 0.3
+logp, adv = torch.randn(rows, device="cuda", generator=g) - 1, torch.randn(rows, device="cuda", generator=g)
+ret, val = torch.randn(rows, device="cuda", generator=g), torch.randn(rows, device="cuda", generator=g)
+ls = torch.zeros(1, 2, device="cuda")
+for actor, k_out in ((True, 2), (False, 1)):
+    wo = torch.randn(k_out, 256, device="cuda", generator=g) / 16
+    bo = torch.zeros(k_out, device="cuda")
+    kw = dict(act=act, logp=logp, adv=adv, logstd=ls) if actor else dict(ret=ret, val=val, clip_vloss=True)
+    launches, per = timed(lambda: U.linear_tanh_loss_x6(x3, w3, b3, wo, bo, real, actor, planes=p3, defer=[], **kw))
+    tf = 2.0 * rows * 256 * 512 / (per * 1e-3) / 1e12
+    print(json.dumps({"stage": f"product vss_linear_tanh_loss_bf16x6 512->256 {'actor' if actor else 'critic'}",
+                      "launches": launches, "ms_per_launch": per, "x6_tflops": tf,
+                      "frac_of_x6_peak": tf / (2500.0 / 6)}), flush=True)

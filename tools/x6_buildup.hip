@@ -24,7 +24,8 @@
 // Variants of a stage (template V, bits): 1 plain instead of nontemporal epilogue stores; 2 the next item's K tile 1
 // weight DMA issued before the epilogue; 4 two MFMA tiles per store as 8 whole 128-B rows (kept in the product);
 // 8 the five smaller products into a per-row-of-tiles temporary added in fp32 (numerics variant 5 of
-// tools/x6_accum_probe.hip); 16 hi.hi into fresh temporaries (variant 7).
+// tools/x6_accum_probe.hip); 16 hi.hi into fresh temporaries (variant 7).  Argument t: the stagger variant (block
+// groups started some microseconds apart, so that their epilogues' HBM bursts interleave).
 //
 //   hipcc -O3 --offload-arch=gfx950 -o tools/_build/x6_buildup tools/x6_buildup.hip
 //   tools/_build/x6_buildup [stage ...] [v] [l] [s]    -> one JSON line per stage / variant
@@ -87,7 +88,7 @@ template <int S, int V>
 __global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __restrict__ q, const char* __restrict__ pimg,
                                                              const float* __restrict__ y, float* __restrict__ out,
                                                              float* __restrict__ partial, float* __restrict__ sinkbuf,
-                                                             uint64_t* __restrict__ stamps) {
+                                                             uint64_t* __restrict__ stamps, int sg, int sd) {
   __shared__ __attribute__((aligned(16))) char lds[LDS + WJ * BI * 4];
   float* cs_lds = reinterpret_cast<float*>(lds + LDS);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wi = wv / WJ, wj = wv % WJ;
@@ -230,6 +231,12 @@ __global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __rest
   gload(r1);
   gload(r0);
   __syncthreads();
+  if (sd > 0) {
+    // the stagger variant: block group slot % sg starts (slot % sg) x sd ticks (100 MHz) late, so that the groups'
+    // epilogues (stores, y loads) stop landing on HBM all at once
+    const uint64_t ts = __builtin_amdgcn_s_memrealtime(), until = (uint64_t)(slot % sg) * (uint64_t)sd;
+    while (__builtin_amdgcn_s_memrealtime() - ts < until) __builtin_amdgcn_s_sleep(2);
+  }
   const uint64_t t0 = __builtin_amdgcn_s_memtime(), c0 = __builtin_amdgcn_s_memrealtime();
   for (int w = slot; w < ITEMS; w += G) {
     const bool has_next = w + G < ITEMS;
@@ -358,6 +365,8 @@ __global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __rest
     }                                                         \
   } while (0)
 
+static int g_sg = 1, g_sd = 0;  // the stagger variant's groups and delay per group (ticks of 10 ns)
+
 struct Bufs {
   float *q, *y, *out, *partial, *sink;
   char* pimg;
@@ -368,7 +377,7 @@ template <int S, int V = 0>
 static void run(const char* name, const Bufs& b) {
   auto launch = [&] {
     hipLaunchKernelGGL((buildup_kernel<S, V>), dim3(GRID), dim3(THREADS), 0, 0, b.q, b.pimg, b.y, b.out, b.partial, b.sink,
-                       b.stamps);
+                       b.stamps, g_sg, g_sd);
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -435,13 +444,14 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   // arguments: stage numbers 0..5, or "v" for the stage-4/5 variants (V: 1 = plain stores instead of nontemporal,
   // 2 = the next item's K tile 1 DMA before the epilogue)
-  bool want[6] = {true, true, true, true, true, true}, variants = false, lines = false, split = false;
+  bool want[6] = {true, true, true, true, true, true}, variants = false, lines = false, split = false, stagger = false;
   if (argc > 1) {
     for (int s = 0; s < 6; ++s) want[s] = false;
     for (int a = 1; a < argc; ++a) {
       if (argv[a][0] == 'v') variants = true;
       else if (argv[a][0] == 'l') lines = true;
       else if (argv[a][0] == 's') split = true;
+      else if (argv[a][0] == 't') stagger = true;
       else want[atoi(argv[a]) % 6] = true;
     }
   }
@@ -469,6 +479,20 @@ int main(int argc, char** argv) {
     run<5, 4>("5 product work, 128-B line stores", b);
     run<0, 16>("0 lds, hi.hi into fresh temporaries", b);
     run<5, 20>("5 product work, hi.hi into fresh temporaries + 128-B line stores", b);
+  }
+  if (stagger) {
+    const int cases[][2] = {{1, 0}, {2, 300}, {4, 150}, {4, 300}, {4, 600}, {8, 150}, {8, 300}, {1, 0}};
+    for (const auto& c : cases) {
+      g_sg = c[0];
+      g_sd = c[1];
+      char name[128];
+      snprintf(name, sizeof name, "5 +y, line stores, stagger %d groups x %d us", c[0], c[1] / 100);
+      run<5, 4>(name, b);
+      snprintf(name, sizeof name, "4 +store, line stores, stagger %d groups x %d us", c[0], c[1] / 100);
+      run<4, 4>(name, b);
+    }
+    g_sg = 1;
+    g_sd = 0;
   }
   if (lines) {
     run<4, 4>("4 +store, 128-B line stores (nt)", b);

@@ -312,9 +312,11 @@ def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
     from vss_amd import minibatch as MB, mlp as M
     args = P.parse_args(["--env-id", "sa", "--num-envs", str(n_envs), "--num-updates", str(updates),
                          "--log", "false", "--seed", "1"])
+    torch.cuda.reset_peak_memory_stats(dev)
     t0 = time.perf_counter()
     _, hist = P.train(args)
     call_s = time.perf_counter() - t0
+    mem = device_memory(dev)
     last = hist[-1]
     red = dev if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu"
     roll_s, upd_s, call_s = reduce_max([last["rollout_s"], last["update_s"], call_s], red)
@@ -367,7 +369,18 @@ def ppo_wallclock(n_envs: int, updates: int, dev, world: int = 1) -> dict:
                               "warmup_kernels), so the runtime's first-use code-object loading of the loop's kernels "
                               "happens before the clock; RNG states restored, training unchanged"
                               if getattr(args, "kernel_warmup", False) else "off"),
-            "projected_wallclock_to_1e8_steps_s": updates_1e8 * per_update, "updates_to_1e8": updates_1e8}
+            "projected_wallclock_to_1e8_steps_s": updates_1e8 * per_update, "updates_to_1e8": updates_1e8,
+            "device_memory": mem}
+
+
+def device_memory(dev) -> dict:
+    """This rank's device memory after a leg: the caching allocator's peaks over the leg (the minibatch graph's
+    pool included) and the device's free memory as the driver reports it (all processes on the device)."""
+    free, total = torch.cuda.mem_get_info(dev)
+    return {"max_reserved_gib": torch.cuda.max_memory_reserved(dev) / 2 ** 30,
+            "max_allocated_gib": torch.cuda.max_memory_allocated(dev) / 2 ** 30,
+            "reserved_gib_after": torch.cuda.memory_reserved(dev) / 2 ** 30,
+            "device_free_gib_after": free / 2 ** 30, "device_total_gib": total / 2 ** 30}
 
 
 def ppo_dma_leg(n_fields: int, updates: int, dev, world: int = 1) -> dict:
@@ -377,7 +390,9 @@ def ppo_dma_leg(n_fields: int, updates: int, dev, world: int = 1) -> dict:
     import ppo_continuous_action_isaacgym as P
     args = P.parse_args(["--env-id", "dma", "--num-envs", str(3 * n_fields), "--num-updates", str(updates),
                          "--log", "false", "--seed", "1"])
+    torch.cuda.reset_peak_memory_stats(dev)
     _, hist = P.train(args)
+    mem = device_memory(dev)
     last = hist[-1]
     red = dev if dist.is_initialized() and dist.get_backend() == "nccl" else "cpu"
     roll_s, upd_s, first_upd_s = reduce_max([last["rollout_s"], last["update_s"], hist[0]["update_s"]], red)
@@ -397,7 +412,8 @@ def ppo_dma_leg(n_fields: int, updates: int, dev, world: int = 1) -> dict:
                                   "one memory pool) against the last one's update_s"),
             "rollout_agent_steps_per_s": rows * args.num_steps / roll_s,
             "train_agent_steps_per_s": rows * args.num_steps / (roll_s + upd_s),
-            "mean_return_last": last["mean_return"], "v_loss_last": last["v_loss"], "entropy_last": last["entropy"]}
+            "mean_return_last": last["mean_return"], "v_loss_last": last["v_loss"], "entropy_last": last["entropy"],
+            "update_s_per_update": [h["update_s"] for h in hist], "device_memory": mem}
 
 
 def update_gemm_roofline(dev, rows: int = 2097152, reps: int = 10) -> dict:

@@ -481,12 +481,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if args.share_gpu else int(os.environ.get("LOCAL_RANK", "0"))
+    # the rank's device first, so that nothing (the process group's set-up included) creates a context or a
+    # queue on another rank's GPU
+    torch.cuda.set_device(local)
     if world > 1:
         if args.dist_backend == "nccl":  # RCCL on ROCm
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
             dist.init_process_group(args.dist_backend)
-    torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
 
     from envs.vss import VSS, default_cfg

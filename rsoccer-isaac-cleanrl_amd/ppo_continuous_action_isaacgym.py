@@ -288,12 +288,12 @@ def setup_distributed():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = local_device_index()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)  # before the process group: nothing touches another rank's GPU
     if world > 1 and not dist.is_initialized():
         backend = os.environ.get("VSS_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         kw = {"device_id": torch.device(f"cuda:{local}")} if backend == "nccl" else {}
         dist.init_process_group(backend, **kw)
-    if torch.cuda.is_available():
-        torch.cuda.set_device(local)
     return world, rank, local
 
 

@@ -332,6 +332,11 @@ class MinibatchGraph:
         self.replays = 0
         self.failed = False  # a self-check found the replay differing from eager: eager from then on
         self.pool = torch.cuda.MemPool() if SHARED_POOL and torch.device(device).type == "cuda" else None
+        # the eager minibatches and the capture on ONE stream: the caching allocator hands a freed block only to
+        # allocations on the stream it was freed on, so with the eager runs on the current stream and the capture
+        # on torch.cuda.graph's own one the pool held two copies of the minibatch (216 of 232 GiB reserved against
+        # a 109 GiB peak of live tensors for DMA config 4, profiles/r06zd_memory_dma.log)
+        self.stream = torch.cuda.Stream(device=device) if self.pool is not None else None
 
     def _body(self):
         if self.direct:
@@ -345,12 +350,16 @@ class MinibatchGraph:
         return tuple(t.detach() for t in st)
 
     def _eager(self):
-        """The minibatch eagerly, its intermediates from the graph's pool (freed at return, reused by the
-        next replay or eager run in stream order)."""
+        """The minibatch eagerly, its intermediates from the graph's pool on the capture's stream (freed at
+        return, reused by the capture, the replays and the next eager run in stream order)."""
         if self.pool is None:
             return self._body()
-        with torch.cuda.use_mem_pool(self.pool):
-            return self._body()
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream), torch.cuda.use_mem_pool(self.pool):
+            out = self._body()
+        cur.wait_stream(self.stream)
+        return out
 
     def _capture(self):
         torch.cuda.synchronize()
@@ -364,7 +373,7 @@ class MinibatchGraph:
         g = torch.cuda.CUDAGraph()
         # thread_local: with several ranks, RCCL's and the process group's own threads keep querying
         # their streams and events while this thread captures (no collective is captured)
-        with torch.cuda.graph(g, pool=self.pool.id if self.pool is not None else None,
+        with torch.cuda.graph(g, pool=self.pool.id if self.pool is not None else None, stream=self.stream,
                               capture_error_mode="thread_local"):
             self.out = self._body()
         self.graph = g

@@ -241,6 +241,32 @@ def test_minibatch_graph_update_equals_eager_gpu(n, nmb, epochs, updates, norm_a
             assert {k: float(v) for k, v in a.items()} == {k: float(v) for k, v in b.items()}
 
 
+@pytest.mark.gpu
+def test_minibatch_graph_pool_holds_one_minibatch_gpu():
+    """MinibatchGraph.prepare runs the eager first minibatch and the capture in ONE memory pool on ONE stream,
+    so the pool holds one minibatch's intermediates: with the eager run on another stream than the capture the
+    caching allocator could not hand the eager run's freed blocks to the capture, and the pool held two copies
+    (DMA config 4: 216 GiB of pool for a 109 GiB peak, profiles/r06zd_memory_dma.log).  Here: the pool's
+    reserved bytes after prepare against the peak of live bytes the prepare reached."""
+    n, nmb = 4 * 262144, 4
+    args = _args(norm_adv=True, clip_vloss=False, num_minibatches=nmb, update_epochs=1)
+    agent = make_agent(2).cuda()
+    flat = P.FlatGrads(agent)
+    graph = P.make_minibatch_graph(agent, flat, args, n, (52,), (2,), "cuda")
+    assert graph is not None and graph.pool is not None
+    z, obs, act = torch.zeros(n, device="cuda"), torch.zeros(n, 52, device="cuda"), torch.zeros(n, 2, device="cuda")
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    graph.prepare(obs, act, z, z, z, z)
+    torch.cuda.synchronize()
+    live_peak = torch.cuda.max_memory_allocated() - base
+    pool = sum(seg["total_size"] for seg in torch.cuda.memory_snapshot()
+               if tuple(seg.get("segment_pool_id", ())) == tuple(graph.pool.id))
+    assert graph.graph is not None and live_peak > 2 ** 30
+    assert pool < 1.3 * live_peak, (pool / 2 ** 30, live_peak / 2 ** 30)
+
+
 def test_graph_check_schedule_is_geometric():
     """The captured minibatch is re-checked against eager at replays 12, 48, 192, ... (not once)."""
     due = [r for r in range(1, 4000) if MB.graph_check_due(r)]

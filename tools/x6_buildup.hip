@@ -25,7 +25,8 @@
 // weight DMA issued before the epilogue; 4 two MFMA tiles per store as 8 whole 128-B rows (kept in the product);
 // 8 the five smaller products into a per-row-of-tiles temporary added in fp32 (numerics variant 5 of
 // tools/x6_accum_probe.hip); 16 hi.hi into fresh temporaries (variant 7).  Argument t: the stagger variant (block
-// groups started some microseconds apart, so that their epilogues' HBM bursts interleave).
+// groups started some microseconds apart, so that their epilogues' HBM bursts interleave); y: bit 32, the epilogue's
+// other y row groups requested before the K loop's last barrier.
 //
 //   hipcc -O3 --offload-arch=gfx950 -o tools/_build/x6_buildup tools/x6_buildup.hip
 //   tools/_build/x6_buildup [stage ...] [v] [l] [s]    -> one JSON line per stage / variant
@@ -36,6 +37,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -247,8 +249,16 @@ __global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __rest
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     f32x4 ypre[TI];
+    f32x4 yrest[TJ][TI];
     const int64_t jb = (int64_t)jt * BJ + wj * WTJ;
     const int ib = it * BI + wi * WTI;
+    auto load_yrest = [&] {
+#pragma unroll
+      for (int j = 1; j < TJ; ++j)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+          yrest[j][i] = *reinterpret_cast<const f32x4*>(y + (jb + 16 * j + fr) * LDO + ib + 16 * i + 4 * fg);
+    };
     for (int kt = 0; kt < KTILES; kt += 2) {
       if constexpr (S >= 5) {
         if (kt + 2 >= KTILES) {
@@ -266,6 +276,16 @@ __global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __rest
         if (kt + 2 < KTILES) dma_p(kt + 2, 0);
         else if (has_next) dma_p(0, 0);
       });
+      if (!(V & 32) || kt + 2 < KTILES) {
+        swrite(r0, 0);
+        __syncthreads();
+        gload(r0);
+      }
+    }
+    if constexpr (V & 32) {
+      // the epilogue's other y row groups requested before the K loop's last barrier (the fragment registers
+      // are free here), so their latency overlaps that barrier's wait for the next item's first tiles
+      if constexpr (S >= 5) load_yrest();
       swrite(r0, 0);
       __syncthreads();
       gload(r0);
@@ -277,14 +297,7 @@ __global__ __launch_bounds__(THREADS, 1) void buildup_kernel(const float* __rest
       float cs[TI][4];
 #pragma unroll
       for (int i = 0; i < TI; ++i) cs[i][0] = cs[i][1] = cs[i][2] = cs[i][3] = 0.f;
-      f32x4 yrest[TJ][TI];
-      if constexpr (S >= 5) {
-#pragma unroll
-        for (int j = 1; j < TJ; ++j)
-#pragma unroll
-          for (int i = 0; i < TI; ++i)
-            yrest[j][i] = *reinterpret_cast<const f32x4*>(y + (jb + 16 * j + fr) * LDO + ib + 16 * i + 4 * fg);
-      }
+      if constexpr (S >= 5 && !(V & 32)) load_yrest();
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int64_t jg = jb + 16 * j + fr;
@@ -444,7 +457,8 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   // arguments: stage numbers 0..5, or "v" for the stage-4/5 variants (V: 1 = plain stores instead of nontemporal,
   // 2 = the next item's K tile 1 DMA before the epilogue)
-  bool want[6] = {true, true, true, true, true, true}, variants = false, lines = false, split = false, stagger = false;
+  bool want[6] = {true, true, true, true, true, true}, variants = false, lines = false, split = false, stagger = false,
+       early_y = false;
   if (argc > 1) {
     for (int s = 0; s < 6; ++s) want[s] = false;
     for (int a = 1; a < argc; ++a) {
@@ -452,6 +466,7 @@ int main(int argc, char** argv) {
       else if (argv[a][0] == 'l') lines = true;
       else if (argv[a][0] == 's') split = true;
       else if (argv[a][0] == 't') stagger = true;
+      else if (argv[a][0] == 'y') early_y = true;
       else want[atoi(argv[a]) % 6] = true;
     }
   }
@@ -479,6 +494,12 @@ int main(int argc, char** argv) {
     run<5, 4>("5 product work, 128-B line stores", b);
     run<0, 16>("0 lds, hi.hi into fresh temporaries", b);
     run<5, 20>("5 product work, hi.hi into fresh temporaries + 128-B line stores", b);
+  }
+  if (early_y) {
+    for (int rep = 0; rep < 2; ++rep) {
+      run<5, 4>("5 +y, line stores (the product)", b);
+      run<5, 36>("5 +y, line stores, other y groups before the last K barrier", b);
+    }
   }
   if (stagger) {
     const int cases[][2] = {{1, 0}, {2, 300}, {4, 150}, {4, 300}, {4, 600}, {8, 150}, {8, 300}, {1, 0}};
